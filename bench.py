@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X batched NMPC solve path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--horizon 30]
+
+One "step" = one cold-started batched SQP solve of B independent cfg#2 instances (2-link arm,
+nx=4, nu=2, N=30, h=2 ms, fp64), i.e. what the reference does per control tick in
+ModelControl::calc_u (src/Mahi/Mpc/ModelControl.cpp:116-172) -- from V = 0 with x_0 pinned, the
+reference's first-call state -- for B instances at once.  Inputs are generated on the device from
+(seed, global instance index) before the timed region (weak scaling: every rank solves its own
+B instances; results are independent of the GPU count).
+
+Prints ONE JSON line on rank 0 (driver contract) with two extra objects:
+  roofline      achieved algorithmic FP64 rate of the fused SQP kernel vs the MI355X FP64 peak,
+                kernel time from HIP events on the launch stream;
+  cpu_baseline  the oracle/ CPU restatement (same GN-SQP, fp64) on a bounded sample, rank 0 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "mahi-mpc_amd"))
+
+METRIC = "MPC solves/sec (whole node), nx=4 N=30 batch, at 1/2/4/8 MI355X"
+SEED = 20250213
+WEIGHTS = [10.0, 1.0, 5.0, 5.0, 5.0, 5.0, 0.01, 0.01]
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector = FP64 matrix peak (AMD spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU (cfg#2: 4096)")
+    ap.add_argument("--horizon", type=int, default=30)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
+                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py), if present")
+    return ap.parse_args()
+
+
+def cpu_baseline(N, h, target_s):
+    """Oracle (oracle/liboracle.so, the same GN-SQP in plain C + OpenMP) on a bounded sample."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as o
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    w = np.array(WEIGHTS)
+    n0 = 4 * threads
+    x0, up, tr = o.synth(SEED, 0, n0, N, h)
+    t = time.perf_counter()
+    o.solve_batch(N, h, x0, up, tr, w, nthreads=threads)
+    dt = time.perf_counter() - t
+    n = int(max(n0, min(200000, n0 * target_s / max(dt, 1e-6))))
+    x0, up, tr = o.synth(SEED, 0, n, N, h)
+    t = time.perf_counter()
+    r = o.solve_batch(N, h, x0, up, tr, w, nthreads=threads)
+    dt = time.perf_counter() - t
+    return dict(value=n / dt, unit="solves/s", cores=threads, kind="port",
+                sample=f"first {n} cfg#2 instances (seed {SEED}), cold start, {dt:.1f} s wall, "
+                       f"{int((r['status'] == 0).sum())}/{n} converged, oracle dense GN-SQP, "
+                       f"{threads} OpenMP threads")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import mmpc
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, N, h_us = args.batch, args.horizon, 2000
+    h = h_us * 1e-6
+
+    tmpdir = tempfile.mkdtemp(prefix="mmpc_bench_")
+    path = mmpc.write_model_json(os.path.join(tmpdir, "nonlinear_double_pendulum.json"),
+                                 "nonlinear_double_pendulum", 4, 2, h_us, N)
+    solver = mmpc.Solver(path, device=local)
+    NV = solver.NV
+    f64 = dict(dtype=torch.float64, device=dev)
+    x0 = torch.empty((B, 4), **f64)
+    up = torch.empty((B, 2), **f64)
+    tr = torch.empty((B, N, 4), **f64)
+    w = torch.tensor(WEIGHTS, **f64)
+    V = torch.zeros((B, NV), **f64)
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    kkt = torch.empty(B, **f64)
+    stream = torch.cuda.current_stream(dev)
+    solver.synth(SEED, rank * B, B, x0, up, tr, stream=stream.cuda_stream)
+
+    def step():
+        V.zero_()   # cold start (reference first call: v_init = 0, ModelControl.cpp:29-50)
+        solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        V.zero_()
+        ev[k][0].record(stream)
+        solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=stream.cuda_stream)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    iters = it.cpu().numpy()
+    status = st.cpu().numpy()
+    conv = int((status == 0).sum())
+    if world > 1:
+        c = torch.tensor([conv], dtype=torch.int64, device=dev)
+        dist.all_reduce(c)
+        conv = int(c.item())
+    total = B * world * args.steps
+    value = total / elapsed
+    fl = mmpc.flops_per_iteration(N)
+    flops_launch = float(iters.sum()) * fl["total"]            # this rank's kernel, algorithmic
+    achieved = flops_launch / (kern_ms * 1e-3) / 1e12
+    survey_fl = float(iters.sum()) * mmpc.survey_flops_per_iteration(N)
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("batch") == B and tj.get("horizon") == N:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: counter-based splitmix64 cfg#2 instances (SURVEY.md 8d), generated on device",
+        "config": {"workload": "cfg#2: 2-link arm nx=4 nu=2, N=30, h=2 ms, cold-start GN-SQP to "
+                               "||grad||<=1e-8, ||g||<=1e-10", "batch_per_gpu": B, "global_batch": B * world,
+                   "horizon": N, "parallelism": f"batch-shard x{world} (no data-path collective)"},
+        "converged": conv,
+        "mean_sqp_iters": float(iters.mean()),
+        "kernel_ms": kern_ms,
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "kernel": "sqp_wave_kernel<TwoLinkArm,30>",
+                     "flops_per_iter": fl["total"],
+                     "survey_8d_equivalent_tflops": survey_fl / (kern_ms * 1e-3) / 1e12},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(N, h, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,157 @@
+/*
+ * mmpc.h -- C-ABI of the MI355X-native batched nonlinear-MPC solve path.
+ *
+ * This is the drop-in boundary for mahi-mpc's hot path.  Each entry point names
+ * the reference interface it replaces (paths relative to the mahi-mpc tree):
+ *
+ *   mmpc_create / mmpc_create_from_json
+ *       replaces ModelControl::load_model  (src/Mahi/Mpc/ModelControl.cpp:21-73):
+ *       reads the <name>.json written by ModelGenerator::save_param_file
+ *       (src/Mahi/Mpc/ModelGenerator.cpp:261-270; schema ModelParameters.cpp:37-72)
+ *       instead of dlopen'ing the CasADi-generated <name>.so via nlpsol(...).
+ *   mmpc_solve_batch / mmpc_solve_batch_host
+ *       replaces `m_solver_result = m_solver(m_solver_args);`
+ *       (src/Mahi/Mpc/ModelControl.cpp:159) -- the IPOPT call over the CasADi NLP
+ *       evaluators -- for B independent instances at once, including the
+ *       per-step linearisation of ModelControl.cpp:125-135 in linear mode.
+ *   mmpc_linearize_batch
+ *       replaces the CasADi externals <name>_get_A / _get_B / _get_x_dot_init
+ *       (ModelGenerator.cpp:51-53, loaded at ModelControl.cpp:70-72; used by the
+ *       examples' plant model, examples/model_control_example.cpp:81-82).
+ *       A and B are returned COLUMN-major, as CasADi DM -> std::vector does.
+ *   mmpc_nlp_eval_batch
+ *       replaces the nlp_f / nlp_g evaluators of the generated <name>.so
+ *       (ModelGenerator.cpp:206-222, generated at :238).
+ *
+ * Conventions.
+ *   - All sizes are int64_t, all arithmetic fp64.
+ *   - Layouts are instance-major ("array of instances"), reference order inside:
+ *       x0[B][nx], u_prev[B][nu], traj[B][N][nx]   (traj row k = target of F(x_k,u_k),
+ *       ModelGenerator.cpp:207-211), weights = (Q[nx] | R[nu] | Rm[nu]) shared
+ *       (weights_stride 0) or per instance (weights_stride = nx+2nu),
+ *       V[B][NV] with V = [x0,u0,x1,u1,...,x_{N-1},u_{N-1},x_N] (ModelGenerator.cpp:61-112).
+ *   - V_inout is the primal warm start on entry (the reference keeps the previous
+ *     solution as x0 for the next call, ModelControl.cpp:160-161; first call = zeros,
+ *     ModelControl.cpp:29-50) and the solution on exit.  V[b][0:nx] is pinned to x0[b]
+ *     as the reference pins x_0 through lbx = ubx = state (ModelControl.cpp:144-145).
+ *   - mmpc_solve_batch takes DEVICE pointers and is stream-ordered on `stream`
+ *     (a hipStream_t; NULL = default stream).  It never allocates and never
+ *     synchronises.  mmpc_solve_batch_host takes host pointers and is synchronous.
+ *   - Functions return MMPC_OK (0) or a negative mmpc_result and never throw.
+ *     Non-convergence is NOT an API error: it is reported per instance in
+ *     status[] (the reference silently uses non-converged IPOPT output,
+ *     ModelControl.cpp:159-163; callers here can see it).
+ *   - A handle may be used from several threads only on distinct streams and only
+ *     for the device-pointer entry points; the _host entry points serialise on an
+ *     internal mutex.
+ */
+#ifndef MMPC_H
+#define MMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMPC_ABI_VERSION 1
+
+typedef struct mmpc_handle mmpc_handle;
+
+/* API result codes (return values) */
+enum mmpc_result {
+    MMPC_OK = 0,
+    MMPC_ERR_INVALID_ARG = -1,
+    MMPC_ERR_IO = -2,
+    MMPC_ERR_PARSE = -3,
+    MMPC_ERR_UNSUPPORTED = -4,
+    MMPC_ERR_HIP = -5,
+    MMPC_ERR_NO_DEVICE = -6
+};
+
+/* per-instance solver status (status[] outputs) */
+enum mmpc_status {
+    MMPC_STATUS_CONVERGED = 0,            /* ||grad||_inf <= tol_grad and ||g||_inf <= tol_defect */
+    MMPC_STATUS_MAX_ITER = 1,             /* opts.max_iter SQP iterations without convergence */
+    MMPC_STATUS_LINESEARCH_FAILED = 2,    /* no sufficient merit decrease after 30 halvings */
+    MMPC_STATUS_NONFINITE = 3,            /* NaN/Inf in the iterate or the KKT residual */
+    MMPC_STATUS_FACTORIZATION_FAILED = 4, /* condensed Hessian not positive definite */
+    MMPC_STATUS_BOUNDS_VIOLATED = 5       /* converged, but the solution leaves a finite u bound
+                                             (box constraints are not active-set handled yet) */
+};
+
+/* built-in dynamics (device code; see DESIGN.md "Models") */
+enum mmpc_model_id {
+    MMPC_MODEL_TWO_LINK_ARM = 0 /* examples/ex_model_generate.cpp:24-43, nx=4 nu=2 */
+};
+
+typedef struct mmpc_opts {
+    int32_t max_iter;   /* SQP iteration cap (reference IPOPT: 200, ModelControl.cpp:55). default 50 */
+    int32_t device;     /* HIP device ordinal; -1 = the calling thread's current device. default -1 */
+    double tol_grad;    /* ||grad_u J_reduced||_inf stop tolerance. default 1e-8 */
+    double tol_defect;  /* ||g||_inf stop tolerance. default 1e-10 */
+} mmpc_opts;
+
+typedef struct mmpc_model_info {
+    char name[128];
+    int32_t model_id;           /* enum mmpc_model_id */
+    int32_t num_x, num_u;       /* nx, nu */
+    int32_t num_shooting_nodes; /* N */
+    int32_t num_v;              /* NV = nx(N+1) + nu N */
+    int32_t num_g;              /* NG = nx N */
+    int32_t is_linear;
+    double step_size;           /* h [s] */
+    int64_t timespan_us;        /* h N in microseconds, as serialised */
+    int64_t step_size_us;
+    double u_min[16], u_max[16], x_min[16], x_max[16]; /* first nu / nx entries valid */
+} mmpc_model_info;
+
+int mmpc_abi_version(void);
+void mmpc_default_opts(mmpc_opts* opts);
+
+/* load <name>.json (ModelParameters schema); opts may be NULL (defaults) */
+int mmpc_create(const char* model_json_path, const mmpc_opts* opts, mmpc_handle** out);
+int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_handle** out);
+int mmpc_destroy(mmpc_handle* h);
+int mmpc_get_model_info(const mmpc_handle* h, mmpc_model_info* info);
+int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts);
+
+/* Batched SQP solve, DEVICE pointers, stream-ordered.  u_lb/u_ub: device [nu] or NULL
+ * (unbounded; |bound| >= 1e19 is unbounded as in IPOPT).  status/iters/kkt_res: device
+ * [B] outputs, each may be NULL. */
+int mmpc_solve_batch(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev,
+                     const double* traj, const double* weights, int64_t weights_stride,
+                     const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
+                     int32_t* iters, double* kkt_res, void* stream);
+
+/* Same contract with HOST pointers; synchronous (H2D, solve, D2H on an internal stream). */
+int mmpc_solve_batch_host(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev,
+                          const double* traj, const double* weights, int64_t weights_stride,
+                          const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
+                          int32_t* iters, double* kkt_res);
+
+/* Continuous-time linearisation at (x[b], u[b]): A = df/dx [nx*nx], B = df/du [nx*nu]
+ * column-major, xdot = f(x,u) [nx].  DEVICE pointers; any output may be NULL. */
+int mmpc_linearize_batch(mmpc_handle* h, int64_t B, const double* x, const double* u,
+                         double* A_colmajor, double* B_colmajor, double* xdot, void* stream);
+int mmpc_linearize_batch_host(mmpc_handle* h, int64_t B, const double* x, const double* u,
+                              double* A_colmajor, double* B_colmajor, double* xdot);
+
+/* NLP value at V: J (ModelGenerator.cpp:208-222) and max |g| (g of :206).  DEVICE pointers. */
+int mmpc_nlp_eval_batch(mmpc_handle* h, int64_t B, const double* V, const double* u_prev,
+                        const double* traj, const double* weights, int64_t weights_stride,
+                        double* J, double* defect_inf, void* stream);
+
+/* Synthetic cfg#2 instances: counter-based splitmix64(seed, first_index + b),
+ * so shards generate identical instances whatever the GPU count.  DEVICE pointers. */
+int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t B, double* x0,
+                     double* u_prev, double* traj, void* stream);
+
+const char* mmpc_status_string(int32_t status);
+/* thread-local description of the last API error on this thread ("" if none) */
+const char* mmpc_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MMPC_H */

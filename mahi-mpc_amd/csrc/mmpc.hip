@@ -1,0 +1,590 @@
+// mmpc.hip -- C-ABI (include/mmpc.h) of the MI355X batched NMPC solve path.
+//
+// Host side of the drop-in boundary: loads the reference's <name>.json model file
+// (src/Mahi/Mpc/ModelParameters.cpp:52-72 semantics), validates every launch shape on
+// the host, and launches the gfx950 kernels of sqp_wave.h / below.  No CPU fallback
+// exists: every compute entry point runs on the GPU or returns an error.
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/mmpc.h"
+#include "json_lite.h"
+#include "models.h"
+#include "sqp_wave.h"
+
+using namespace mmpc;
+
+// ---------------------------------------------------------------- errors
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+int hip_fail(hipError_t e, const char* where) {
+    return fail(MMPC_ERR_HIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+#define MMPC_HIP(call)                                    \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hip_fail(e_, #call); \
+    } while (0)
+}  // namespace
+
+// ---------------------------------------------------------------- handle
+struct mmpc_handle {
+    mmpc_model_info info;
+    mmpc_opts opts;
+    std::mutex host_mu;  // serialises the *_host entry points
+    hipStream_t host_stream = nullptr;
+    int host_dev = -1;
+    // device staging for the *_host entry points (grown on demand)
+    double* d_buf = nullptr;
+    size_t d_buf_bytes = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    bool changed = false;
+    int err = 0;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) {
+            err = 1;
+            return;
+        }
+        if (dev >= 0 && dev != prev) {
+            if (hipSetDevice(dev) != hipSuccess) {
+                err = 1;
+                return;
+            }
+            changed = true;
+        }
+    }
+    ~DeviceGuard() {
+        if (changed) (void)hipSetDevice(prev);
+    }
+};
+
+int parse_model(const std::string& text, mmpc_model_info* info) {
+    json::Value root;
+    try {
+        root = json::parse(text);
+    } catch (const std::exception& ex) {
+        return fail(MMPC_ERR_PARSE, ex.what());
+    }
+    const json::Value* m = root.get("model");  // ModelGenerator.cpp:264 writes j["model"]
+    if (!m) m = &root;
+    if (m->kind != json::Value::Object) return fail(MMPC_ERR_PARSE, "model entry is not an object");
+    auto num = [&](const char* k, double* out) -> bool {
+        const json::Value* v = m->get(k);
+        if (!v || v->kind != json::Value::Number) return false;
+        *out = v->num;
+        return true;
+    };
+    std::memset(info, 0, sizeof(*info));
+    const json::Value* nm = m->get("name");
+    if (!nm || nm->kind != json::Value::String) return fail(MMPC_ERR_PARSE, "missing \"name\"");
+    std::snprintf(info->name, sizeof(info->name), "%s", nm->str.c_str());
+    double nx, nu, N, step_us, span_us = 0.0;
+    if (!num("num_x", &nx) || !num("num_u", &nu) || !num("num_shooting_nodes", &N) || !num("step_size", &step_us))
+        return fail(MMPC_ERR_PARSE, "missing num_x / num_u / num_shooting_nodes / step_size");
+    num("timespan", &span_us);
+    info->num_x = static_cast<int32_t>(nx);
+    info->num_u = static_cast<int32_t>(nu);
+    info->num_shooting_nodes = static_cast<int32_t>(N);
+    if (info->num_x < 1 || info->num_x > 16 || info->num_u < 1 || info->num_u > 16 || info->num_shooting_nodes < 1)
+        return fail(MMPC_ERR_PARSE, "num_x / num_u / num_shooting_nodes out of range");
+    info->step_size_us = static_cast<int64_t>(std::llround(step_us));
+    info->timespan_us = static_cast<int64_t>(std::llround(span_us));
+    info->step_size = step_us * 1e-6;  // mahi::util::microseconds(j.at("step_size"))
+    info->num_v = info->num_x * (info->num_shooting_nodes + 1) + info->num_u * info->num_shooting_nodes;
+    info->num_g = info->num_x * info->num_shooting_nodes;
+    const json::Value* lin = m->get("is_linear");
+    info->is_linear = (lin && lin->kind == json::Value::Bool && lin->b) ? 1 : 0;
+    // bounds: default +-10e30 (ModelParameters.cpp:21-24); x bounds of exactly +-10e30 become +-inf on
+    // load (ModelParameters.cpp:66-69); nlohmann writes +-inf as null, read back here as unbounded.
+    auto bounds = [&](const char* k, double* out, int n, double dflt, bool inf_map) -> int {
+        for (int i = 0; i < n; ++i) out[i] = dflt;
+        const json::Value* v = m->get(k);
+        if (!v || v->kind == json::Value::Null) return 0;
+        if (v->kind != json::Value::Array) return fail(MMPC_ERR_PARSE, std::string(k) + " is not an array");
+        if (static_cast<int>(v->arr.size()) != n && !v->arr.empty())
+            return fail(MMPC_ERR_PARSE, std::string(k) + " has the wrong length");
+        for (size_t i = 0; i < v->arr.size(); ++i) {
+            const json::Value& e = v->arr[i];
+            if (e.kind == json::Value::Null) out[i] = dflt;
+            else if (e.kind == json::Value::Number) out[i] = e.num;
+            else return fail(MMPC_ERR_PARSE, std::string(k) + " has a non-number entry");
+            if (inf_map && std::fabs(out[i]) == 10e30) out[i] = std::copysign(INFINITY, out[i]);
+        }
+        return 0;
+    };
+    int rc;
+    if ((rc = bounds("x_min", info->x_min, info->num_x, -INFINITY, true))) return rc;
+    if ((rc = bounds("x_max", info->x_max, info->num_x, INFINITY, true))) return rc;
+    if ((rc = bounds("u_min", info->u_min, info->num_u, -10e30, false))) return rc;
+    if ((rc = bounds("u_max", info->u_max, info->num_u, 10e30, false))) return rc;
+    // dynamics: explicit "mmpc_model" key, else the only built-in model with these dimensions
+    const json::Value* mdl = m->get("mmpc_model");
+    if (mdl && mdl->kind == json::Value::String) {
+        if (mdl->str == "two_link_arm" || mdl->str == "double_pendulum") info->model_id = MMPC_MODEL_TWO_LINK_ARM;
+        else return fail(MMPC_ERR_UNSUPPORTED, "unknown mmpc_model \"" + mdl->str + "\"");
+    } else if (info->num_x == 4 && info->num_u == 2) {
+        info->model_id = MMPC_MODEL_TWO_LINK_ARM;
+    } else {
+        return fail(MMPC_ERR_UNSUPPORTED, "no built-in dynamics for these dimensions (set \"mmpc_model\")");
+    }
+    if (info->model_id == MMPC_MODEL_TWO_LINK_ARM && (info->num_x != 4 || info->num_u != 2))
+        return fail(MMPC_ERR_PARSE, "two_link_arm needs num_x = 4, num_u = 2");
+    return MMPC_OK;
+}
+
+int validate_opts(const mmpc_opts* o) {
+    if (o->max_iter < 0 || o->max_iter > 100000) return fail(MMPC_ERR_INVALID_ARG, "max_iter out of range");
+    if (!(o->tol_grad > 0.0) || !(o->tol_defect > 0.0)) return fail(MMPC_ERR_INVALID_ARG, "tolerances must be > 0");
+    return MMPC_OK;
+}
+
+int resolve_device(mmpc_handle* h, int* dev) {
+    if (h->opts.device >= 0) {
+        *dev = h->opts.device;
+        return MMPC_OK;
+    }
+    int d = -1;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess) return fail(MMPC_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
+    *dev = d;
+    return MMPC_OK;
+}
+
+// ---------------------------------------------------------------- auxiliary kernels
+template <class Model>
+__global__ __launch_bounds__(256) void linearize_kernel(int64_t B, const double* __restrict__ x,
+                                                        const double* __restrict__ u, double* A, double* Bm,
+                                                        double* xdot) {
+    constexpr int NX = Model::NX, NU = Model::NU;
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    double xv[NX], uv[NU], xd[NX], fx[NX * NX], fu[NX * NU];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xv[i] = x[b * NX + i];
+#pragma unroll
+    for (int i = 0; i < NU; ++i) uv[i] = u[b * NU + i];
+    model_eval_jac<Model>(xv, uv, xd, fx, fu);
+    // column-major, as CasADi DM -> std::vector (ModelControl.cpp:127-129)
+#pragma unroll
+    for (int r = 0; r < NX; ++r) {
+        if (xdot) xdot[b * NX + r] = xd[r];
+#pragma unroll
+        for (int c = 0; c < NX; ++c)
+            if (A) A[b * NX * NX + c * NX + r] = fx[r * NX + c];
+#pragma unroll
+        for (int c = 0; c < NU; ++c)
+            if (Bm) Bm[b * NX * NU + c * NX + r] = fu[r * NU + c];
+    }
+}
+
+template <class Model>
+__global__ __launch_bounds__(256) void nlp_eval_kernel(int64_t B, int N, double h, int is_linear,
+                                                       const double* __restrict__ V, const double* __restrict__ u_prev,
+                                                       const double* __restrict__ traj,
+                                                       const double* __restrict__ weights, int64_t w_stride,
+                                                       double* J, double* ginf) {
+    constexpr int NX = Model::NX, NU = Model::NU, ND = NX + NU;
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int NV = NX * (N + 1) + NU * N;
+    const double* v = V + b * NV;
+    const double* w = weights + b * w_stride;
+    const double* up = u_prev + b * NU;
+    const double* tr = traj + b * (int64_t)N * NX;
+    double lin[NX * NX + NX * NU + NX];
+    if (is_linear) {  // F_lin at (x*, u*) = (x_0, u_prev), ModelGenerator.cpp:47-48
+        double xd[NX], fx[NX * NX], fu[NX * NU];
+        model_eval_jac<Model>(v, up, xd, fx, fu);
+        for (int i = 0; i < NX * NX; ++i) lin[i] = fx[i];
+        for (int i = 0; i < NX * NU; ++i) lin[NX * NX + i] = fu[i];
+        for (int i = 0; i < NX; ++i) lin[NX * NX + NX * NU + i] = xd[i];
+    }
+    double Jv = 0.0, gm = 0.0;
+    for (int k = 0; k < N; ++k) {
+        const double* xk = v + k * ND;
+        const double* uk = xk + NX;
+        double xd[NX];
+        if (!is_linear) {
+            model_eval<Model>(xk, uk, xd);
+        } else {
+            for (int r = 0; r < NX; ++r) {
+                double s = lin[NX * NX + NX * NU + r];
+                for (int c = 0; c < NX; ++c) s += lin[r * NX + c] * (xk[c] - v[c]);
+                for (int c = 0; c < NU; ++c) s += lin[NX * NX + r * NU + c] * (uk[c] - up[c]);
+                xd[r] = s;
+            }
+        }
+        for (int r = 0; r < NX; ++r) {
+            const double F = xk[r] + h * xd[r];
+            const double e = F - tr[k * NX + r];
+            Jv += e * w[r] * e;
+            const double gk = F - v[(k + 1) * ND + r];
+            gm = (std::fabs(gk) > gm || gk != gk) ? std::fabs(gk) : gm;
+        }
+        for (int c = 0; c < NU; ++c) {
+            const double um = (k == 0) ? up[c] : v[(k - 1) * ND + NX + c];
+            const double du = uk[c] - um;
+            Jv += du * w[NX + c] * du + uk[c] * w[NX + NU + c] * uk[c];
+        }
+    }
+    if (J) J[b] = Jv;
+    if (ginf) ginf[b] = gm;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double unit_draw(uint64_t seed, int64_t index, int j) {
+    const uint64_t v = splitmix64(seed ^ splitmix64((uint64_t)index * 16ull + (uint64_t)j));
+    return (double)(v >> 11) * 0x1.0p-53;
+}
+
+// lo + span*u with an unfused product (bit-identical to the oracle's and make_golden.py's generator)
+__device__ __forceinline__ double affine_draw(double lo, double span, double u) {
+#pragma clang fp contract(off)
+    const double p = span * u;
+    return lo + p;
+}
+
+// SURVEY.md 8d cfg#2 instance generator (identical recipe in oracle/ and tests/golden/)
+__global__ __launch_bounds__(256) void synth_two_link_kernel(uint64_t seed, int64_t first, int64_t B, int N,
+                                                             double h, double* x0, double* u_prev, double* traj) {
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const double PI = 3.14159265358979323846;
+    const int64_t gi = first + b;
+    x0[b * 4 + 0] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 0));
+    x0[b * 4 + 1] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 1));
+    x0[b * 4 + 2] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 2));
+    x0[b * 4 + 3] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 3));
+    u_prev[b * 2 + 0] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 4));
+    u_prev[b * 2 + 1] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 5));
+    const double a = affine_draw(0.5, 0.5, unit_draw(seed, gi, 6));
+    const double f = affine_draw(0.25, 0.75, unit_draw(seed, gi, 7));
+    const double ph = affine_draw(0.0, 2.0 * PI, unit_draw(seed, gi, 8));
+    for (int k = 0; k < N; ++k) {
+        const double arg = 2.0 * PI * f * (k * h) + ph;
+        const double sv = a * sin(arg), cv = 2.0 * PI * f * a * cos(arg);
+        double* r = traj + (b * N + k) * 4;
+        r[0] = sv;
+        r[1] = -sv;
+        r[2] = cv;
+        r[3] = -cv;
+    }
+}
+
+inline unsigned grid1d(int64_t B, int threads) { return static_cast<unsigned>((B + threads - 1) / threads); }
+
+int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
+                 const double* weights, int64_t w_stride, const double* u_lb, const double* u_ub, double* V,
+                 int32_t* status, int32_t* iters, double* kkt, hipStream_t stream) {
+    const mmpc_model_info& mi = h->info;
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!x0 || !u_prev || !traj || !weights || !V) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    const int nw = mi.num_x + 2 * mi.num_u;
+    if (w_stride != 0 && w_stride < nw) return fail(MMPC_ERR_INVALID_ARG, "weights_stride must be 0 or >= nx+2nu");
+    if (B > 0x7fffffffLL) return fail(MMPC_ERR_INVALID_ARG, "B exceeds the grid limit (2^31-1)");
+    SolveParams p;
+    p.B = B;
+    p.N = mi.num_shooting_nodes;
+    p.max_iter = h->opts.max_iter;
+    p.h = mi.step_size;
+    p.tol_grad = h->opts.tol_grad;
+    p.tol_defect = h->opts.tol_defect;
+    p.is_linear = mi.is_linear;
+    p.x0 = x0;
+    p.u_prev = u_prev;
+    p.traj = traj;
+    p.weights = weights;
+    p.w_stride = w_stride;
+    p.u_lb = u_lb;
+    p.u_ub = u_ub;
+    p.V = V;
+    p.status = status;
+    p.iters = iters;
+    p.kkt = kkt;
+    if (mi.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "model not built in");
+    // host-side shape checks: the kernel holds one condensed-Hessian row per lane
+    const int N = mi.num_shooting_nodes;
+    if (N * TwoLinkArm::NU > 64)
+        return fail(MMPC_ERR_UNSUPPORTED, "N*nu > 64: horizon too long for the single-wave kernel");
+    dim3 grid(static_cast<unsigned>(B)), block(64);
+    if (N <= 16) sqp_wave_kernel<TwoLinkArm, 16><<<grid, block, 0, stream>>>(p);
+    else if (N <= 30) sqp_wave_kernel<TwoLinkArm, 30><<<grid, block, 0, stream>>>(p);
+    else sqp_wave_kernel<TwoLinkArm, 32><<<grid, block, 0, stream>>>(p);
+    MMPC_HIP(hipGetLastError());
+    return MMPC_OK;
+}
+
+int ensure_host_ctx(mmpc_handle* h, size_t bytes) {
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    if (h->host_stream && h->host_dev != dev) return fail(MMPC_ERR_INVALID_ARG, "handle used on two devices");
+    if (!h->host_stream) {
+        MMPC_HIP(hipStreamCreateWithFlags(&h->host_stream, hipStreamNonBlocking));
+        h->host_dev = dev;
+    }
+    if (bytes > h->d_buf_bytes) {
+        if (h->d_buf) MMPC_HIP(hipFree(h->d_buf));
+        h->d_buf = nullptr;
+        h->d_buf_bytes = 0;
+        MMPC_HIP(hipMalloc(reinterpret_cast<void**>(&h->d_buf), bytes));
+        h->d_buf_bytes = bytes;
+    }
+    return MMPC_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- C-ABI
+extern "C" {
+
+int mmpc_abi_version(void) { return MMPC_ABI_VERSION; }
+
+void mmpc_default_opts(mmpc_opts* o) {
+    if (!o) return;
+    o->max_iter = 50;
+    o->device = -1;
+    o->tol_grad = 1e-8;
+    o->tol_defect = 1e-10;
+}
+
+int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_handle** out) {
+    if (!json_text || !out) return fail(MMPC_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    mmpc_opts o;
+    mmpc_default_opts(&o);
+    if (opts) o = *opts;
+    int rc = validate_opts(&o);
+    if (rc) return rc;
+    mmpc_model_info info;
+    rc = parse_model(json_text, &info);
+    if (rc) return rc;
+    mmpc_handle* h = new (std::nothrow) mmpc_handle();
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "out of memory");
+    h->info = info;
+    h->opts = o;
+    *out = h;
+    g_last_error.clear();
+    return MMPC_OK;
+}
+
+int mmpc_create(const char* path, const mmpc_opts* opts, mmpc_handle** out) {
+    if (!path || !out) return fail(MMPC_ERR_INVALID_ARG, "null argument");
+    std::ifstream f(path);  // ModelControl.cpp:24 reads <model_name>.json
+    if (!f) return fail(MMPC_ERR_IO, std::string("cannot open ") + path);
+    std::stringstream ss;
+    ss << f.rdbuf();
+    return mmpc_create_from_json(ss.str().c_str(), opts, out);
+}
+
+int mmpc_destroy(mmpc_handle* h) {
+    if (!h) return MMPC_OK;
+    if (h->host_stream || h->d_buf) {
+        DeviceGuard g(h->host_dev);
+        if (h->d_buf) (void)hipFree(h->d_buf);
+        if (h->host_stream) (void)hipStreamDestroy(h->host_stream);
+    }
+    delete h;
+    return MMPC_OK;
+}
+
+int mmpc_get_model_info(const mmpc_handle* h, mmpc_model_info* info) {
+    if (!h || !info) return fail(MMPC_ERR_INVALID_ARG, "null argument");
+    *info = h->info;
+    return MMPC_OK;
+}
+
+int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts) {
+    if (!h || !opts) return fail(MMPC_ERR_INVALID_ARG, "null argument");
+    int rc = validate_opts(opts);
+    if (rc) return rc;
+    h->opts = *opts;
+    return MMPC_OK;
+}
+
+int mmpc_solve_batch(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
+                     const double* weights, int64_t weights_stride, const double* u_lb, const double* u_ub,
+                     double* V_inout, int32_t* status, int32_t* iters, double* kkt_res, void* stream) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!x0 || !u_prev || !traj || !weights || !V_inout) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    return launch_solve(h, B, x0, u_prev, traj, weights, weights_stride, u_lb, u_ub, V_inout, status, iters,
+                        kkt_res, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mmpc_solve_batch_host(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
+                          const double* weights, int64_t weights_stride, const double* u_lb, const double* u_ub,
+                          double* V_inout, int32_t* status, int32_t* iters, double* kkt_res) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!x0 || !u_prev || !traj || !weights || !V_inout) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    std::lock_guard<std::mutex> lk(h->host_mu);
+    const mmpc_model_info& mi = h->info;
+    const size_t nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes, NV = mi.num_v;
+    const size_t nw = nx + 2 * nu;
+    const size_t nW = weights_stride ? (size_t)B * (size_t)weights_stride : nw;
+    // doubles: x0, u_prev, traj, weights, lb, ub, V, kkt ; ints: status, iters (as doubles' room)
+    const size_t off_x0 = 0, off_up = off_x0 + B * nx, off_tr = off_up + B * nu, off_w = off_tr + B * N * nx;
+    const size_t off_lb = off_w + nW, off_ub = off_lb + nu, off_V = off_ub + nu, off_kkt = off_V + B * NV;
+    const size_t off_st = off_kkt + B, off_it = off_st + (B + 1) / 2, total = off_it + (B + 1) / 2;
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    rc = ensure_host_ctx(h, total * sizeof(double));
+    if (rc) return rc;
+    double* d = h->d_buf;
+    hipStream_t s = h->host_stream;
+    MMPC_HIP(hipMemcpyAsync(d + off_x0, x0, B * nx * sizeof(double), hipMemcpyHostToDevice, s));
+    MMPC_HIP(hipMemcpyAsync(d + off_up, u_prev, B * nu * sizeof(double), hipMemcpyHostToDevice, s));
+    MMPC_HIP(hipMemcpyAsync(d + off_tr, traj, B * N * nx * sizeof(double), hipMemcpyHostToDevice, s));
+    MMPC_HIP(hipMemcpyAsync(d + off_w, weights, nW * sizeof(double), hipMemcpyHostToDevice, s));
+    if (u_lb) MMPC_HIP(hipMemcpyAsync(d + off_lb, u_lb, nu * sizeof(double), hipMemcpyHostToDevice, s));
+    if (u_ub) MMPC_HIP(hipMemcpyAsync(d + off_ub, u_ub, nu * sizeof(double), hipMemcpyHostToDevice, s));
+    MMPC_HIP(hipMemcpyAsync(d + off_V, V_inout, B * NV * sizeof(double), hipMemcpyHostToDevice, s));
+    int32_t* dst = reinterpret_cast<int32_t*>(d + off_st);
+    int32_t* dit = reinterpret_cast<int32_t*>(d + off_it);
+    rc = launch_solve(h, B, d + off_x0, d + off_up, d + off_tr, d + off_w, weights_stride, u_lb ? d + off_lb : nullptr,
+                      u_ub ? d + off_ub : nullptr, d + off_V, dst, dit, d + off_kkt, s);
+    if (rc) return rc;
+    MMPC_HIP(hipMemcpyAsync(V_inout, d + off_V, B * NV * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (status) MMPC_HIP(hipMemcpyAsync(status, dst, B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (iters) MMPC_HIP(hipMemcpyAsync(iters, dit, B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (kkt_res) MMPC_HIP(hipMemcpyAsync(kkt_res, d + off_kkt, B * sizeof(double), hipMemcpyDeviceToHost, s));
+    MMPC_HIP(hipStreamSynchronize(s));
+    return MMPC_OK;
+}
+
+int mmpc_linearize_batch(mmpc_handle* h, int64_t B, const double* x, const double* u, double* A_colmajor,
+                         double* B_colmajor, double* xdot, void* stream) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!x || !u) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    if (h->info.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "model not built in");
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    linearize_kernel<TwoLinkArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        B, x, u, A_colmajor, B_colmajor, xdot);
+    MMPC_HIP(hipGetLastError());
+    return MMPC_OK;
+}
+
+int mmpc_linearize_batch_host(mmpc_handle* h, int64_t B, const double* x, const double* u, double* A_colmajor,
+                              double* B_colmajor, double* xdot) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!x || !u) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    std::lock_guard<std::mutex> lk(h->host_mu);
+    const size_t nx = h->info.num_x, nu = h->info.num_u;
+    const size_t off_x = 0, off_u = B * nx, off_A = off_u + B * nu, off_B = off_A + B * nx * nx,
+                 off_f = off_B + B * nx * nu, total = off_f + B * nx;
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    rc = ensure_host_ctx(h, total * sizeof(double));
+    if (rc) return rc;
+    double* d = h->d_buf;
+    hipStream_t s = h->host_stream;
+    MMPC_HIP(hipMemcpyAsync(d + off_x, x, B * nx * sizeof(double), hipMemcpyHostToDevice, s));
+    MMPC_HIP(hipMemcpyAsync(d + off_u, u, B * nu * sizeof(double), hipMemcpyHostToDevice, s));
+    rc = mmpc_linearize_batch(h, B, d + off_x, d + off_u, d + off_A, d + off_B, d + off_f, s);
+    if (rc) return rc;
+    if (A_colmajor) MMPC_HIP(hipMemcpyAsync(A_colmajor, d + off_A, B * nx * nx * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (B_colmajor) MMPC_HIP(hipMemcpyAsync(B_colmajor, d + off_B, B * nx * nu * sizeof(double), hipMemcpyDeviceToHost, s));
+    if (xdot) MMPC_HIP(hipMemcpyAsync(xdot, d + off_f, B * nx * sizeof(double), hipMemcpyDeviceToHost, s));
+    MMPC_HIP(hipStreamSynchronize(s));
+    return MMPC_OK;
+}
+
+int mmpc_nlp_eval_batch(mmpc_handle* h, int64_t B, const double* V, const double* u_prev, const double* traj,
+                        const double* weights, int64_t weights_stride, double* J, double* defect_inf, void* stream) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!V || !u_prev || !traj || !weights) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    if (h->info.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "model not built in");
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    nlp_eval_kernel<TwoLinkArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
+        weights_stride, J, defect_inf);
+    MMPC_HIP(hipGetLastError());
+    return MMPC_OK;
+}
+
+int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t B, double* x0, double* u_prev,
+                     double* traj, void* stream) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    if (B < 0 || first_index < 0) return fail(MMPC_ERR_INVALID_ARG, "negative B / first_index");
+    if (B == 0) return MMPC_OK;
+    if (!x0 || !u_prev || !traj) return fail(MMPC_ERR_INVALID_ARG, "null output pointer");
+    if (h->info.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "generator is cfg#2 only");
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    synth_two_link_kernel<<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
+    MMPC_HIP(hipGetLastError());
+    return MMPC_OK;
+}
+
+const char* mmpc_status_string(int32_t s) {
+    switch (s) {
+        case MMPC_STATUS_CONVERGED: return "converged";
+        case MMPC_STATUS_MAX_ITER: return "max_iter";
+        case MMPC_STATUS_LINESEARCH_FAILED: return "linesearch_failed";
+        case MMPC_STATUS_NONFINITE: return "nonfinite";
+        case MMPC_STATUS_FACTORIZATION_FAILED: return "factorization_failed";
+        case MMPC_STATUS_BOUNDS_VIOLATED: return "bounds_violated";
+        default: return "unknown";
+    }
+}
+
+const char* mmpc_last_error(void) { return g_last_error.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,594 @@
+// sqp_wave.h -- fused Gauss-Newton SQP, one 64-lane wavefront per MPC instance.
+//
+// Replaces the IPOPT call `m_solver(m_solver_args)` of src/Mahi/Mpc/ModelControl.cpp:159
+// for the NLP built by src/Mahi/Mpc/ModelGenerator.cpp:23-233 (see DESIGN.md "Solver").
+// Valid for NX == 4 and M = N*NU <= 64 (the condensed Hessian has one row per lane).
+//
+// Per SQP iteration, all inside one workgroup of 64 lanes (no HBM traffic after the
+// initial load; everything lives in LDS and VGPRs):
+//   1. stage evaluation, lane k < N: F_k = x_k + h f(x_k,u_k), A_k = I + h f_x, B_k = h f_u
+//      (forward-mode duals), defects c_k = F_k - x_{k+1}                (ModelGenerator.cpp:33-34, :206)
+//   2. forward d_{k+1} = A_k d_k + c_k and e_k = F_k + A_k d_k - r_k    (quad-DPP, no LDS round trip)
+//   3. adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1}; gradient g = B^T lam + R/Rm terms; stop test
+//   4. Lyapunov P_i = Q + A_i^T P_{i+1} A_i, Z_i = B_i^T P_{i+1}         (16 lanes, LDS)
+//   5. condensed Hessian H = Gamma^T Q Gamma + D^T R D + Rm, one row per lane, built by two
+//      O(N) recursions per row (no Gamma is ever formed):
+//         H_ij = Z_i Phi_{i+1,j+1} B_j (j <= i),   H_ij = (Z_j Phi_{j+1,i+1} B_i)^T (j > i)
+//   6. Gauss-Jordan on [H | -g] with the row in registers; pivot rows are broadcast with
+//      v_readlane and the active window is shifted left each step, so the pivot column
+//      is always register 0 (runtime loop, static register indices)
+//   7. dx_0 = 0, dx_{k+1} = A_k dx_k + B_k du_k + c_k                     (quad-DPP)
+//   8. l1-merit Armijo backtracking, trial stages evaluated in parallel
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "models.h"
+
+#ifndef MMPC_WAVES_PER_SIMD
+#define MMPC_WAVES_PER_SIMD 3
+#endif
+
+namespace mmpc {
+
+struct SolveParams {
+    int64_t B;
+    int N;
+    int max_iter;
+    double h;
+    double tol_grad;
+    double tol_defect;
+    int is_linear;
+    const double* x0;
+    const double* u_prev;
+    const double* traj;
+    const double* weights;
+    int64_t w_stride;
+    const double* u_lb;
+    const double* u_ub;
+    double* V;
+    int32_t* status;
+    int32_t* iters;
+    double* kkt;
+};
+
+enum {
+    ST_CONVERGED = 0,
+    ST_MAX_ITER = 1,
+    ST_LS_FAILED = 2,
+    ST_NONFINITE = 3,
+    ST_FACT_FAILED = 4,
+    ST_BOUNDS = 5
+};
+
+// ---------------- wave helpers ----------------
+// Pin a value at this point of the instruction stream.  Without it the optimiser sinks the
+// unrolled H-build / Gauss-Jordan arithmetic to its final uses and keeps every broadcast
+// operand alive until then (measured: 2.7 KB/lane of scratch spills); with it the kernel
+// fits 3 waves/SIMD with no spills.
+#define MMPC_PIN(x) asm volatile("" : "+v"(x))
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+    return __hiloint2double(hi, lo);
+}
+
+// broadcast lane Q of each quad to the whole quad (DPP quad_perm [Q,Q,Q,Q])
+template <int Q>
+__device__ __forceinline__ double quad_bcast(double v) {
+    constexpr int ctrl = Q | (Q << 2) | (Q << 4) | (Q << 6);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// reciprocal to ~1 ulp: hardware estimate + two Newton steps
+__device__ __forceinline__ double rcp_nr(double a) {
+    double r = __builtin_amdgcn_rcp(a);
+    double e = fma(-a, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-a, r, 1.0);
+    return fma(r, e, r);
+}
+
+// ---------------- the kernel ----------------
+template <class Model, int NMAX>
+__global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(SolveParams p) {
+    constexpr int NX = Model::NX, NU = Model::NU, ND = NX + NU;
+    constexpr int MMAX = NMAX * NU;
+    static_assert(NX == 4, "quad-DPP recursions assume NX == 4");
+    static_assert(MMAX <= 64, "one Hessian row per lane");
+
+    __shared__ double sX[(NMAX + 1) * NX];
+    __shared__ double sU[NMAX * NU];
+    __shared__ double sF[NMAX * NX];
+    __shared__ double sA[NMAX * NX * NX];
+    __shared__ double sB[NMAX * NX * NU];
+    __shared__ double sZ[NMAX * NU * NX];
+    __shared__ double sC[NMAX * NX];
+    __shared__ double sE[NMAX * NX];
+    __shared__ double sR[NMAX * NX];
+    __shared__ double sLam[(NMAX + 1) * NX];
+    __shared__ double sDX[(NMAX + 1) * NX];
+    __shared__ double sDU[MMAX];
+    __shared__ double sP[NX * NX];
+    __shared__ double sT[NX * NX];
+    __shared__ double sW[NX + 2 * NU];
+    __shared__ double sLin[NX * NX + NX * NU + NX];
+    __shared__ double sUp[NU];
+
+    const int lane0 = threadIdx.x;
+    const int lane = lane0;
+    const int64_t inst = blockIdx.x;
+    const int N = p.N;
+    const int M = N * NU;
+    const int NV = NX * (N + 1) + NU * N;
+    const double hstep = p.h;
+
+    // ---- load the instance (the only HBM reads of the solve) ----
+    const double* w = p.weights + inst * p.w_stride;
+    if (lane < NX + 2 * NU) sW[lane] = w[lane];
+    const double* trj = p.traj + inst * (int64_t)N * NX;
+    for (int i = lane; i < N * NX; i += 64) sR[i] = trj[i];
+    const double* Vin = p.V + inst * (int64_t)NV;
+    for (int i = lane; i < NV; i += 64) {
+        const int k = i / ND, r = i - k * ND;
+        const double v = Vin[i];
+        if (k < N) {
+            if (r < NX) sX[k * NX + r] = v;
+            else sU[k * NU + r - NX] = v;
+        } else {
+            sX[N * NX + r] = v;
+        }
+    }
+    // stages >= N are structurally zero in the static-NMAX loops below
+    for (int i = N * NX * NX + lane; i < NMAX * NX * NX; i += 64) sA[i] = 0.0;
+    for (int i = N * NX * NU + lane; i < NMAX * NX * NU; i += 64) {
+        sB[i] = 0.0;
+        sZ[i] = 0.0;
+    }
+    __syncthreads();
+    if (lane < NX) sX[lane] = p.x0[inst * NX + lane];  // x_0 pinned (ModelControl.cpp:144-145)
+    if (lane < NU) sUp[lane] = p.u_prev[inst * NU + lane];
+    __syncthreads();
+    double up[NU];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) up[c] = sUp[c];
+
+    // linear mode: A*, B*, xdot* at (state, control) once per solve (ModelControl.cpp:125-135)
+    if (p.is_linear) {
+        if (lane == 0) {
+            double x[NX], xd[NX], fx[NX * NX], fu[NX * NU];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) x[i] = sX[i];
+            model_eval_jac<Model>(x, up, xd, fx, fu);
+#pragma unroll
+            for (int i = 0; i < NX * NX; ++i) sLin[i] = fx[i];
+#pragma unroll
+            for (int i = 0; i < NX * NU; ++i) sLin[NX * NX + i] = fu[i];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) sLin[NX * NX + NX * NU + i] = xd[i];
+        }
+        __syncthreads();
+    }
+
+    int status = ST_MAX_ITER;
+    int it = 0;
+    double kkt = 0.0, mu = 0.0;
+
+    for (it = 0; it <= p.max_iter; ++it) {
+        // Re-derive the lane id opaquely each iteration: otherwise LICM hoists every lane-dependent
+        // compare mask and LDS address of the unrolled phases out of this loop (hundreds of SGPR
+        // pairs -> spills).  Recomputing them costs a few SALU/VALU ops per iteration.
+        int lane = lane0;
+        asm volatile("" : "+v"(lane));
+        const int qa = lane & 3;  // quad lane = state row index for the vector recursions
+        // ---- 1. stage evaluation ----
+        double cmax = 0.0;
+        bool nonfinite = false;
+        if (lane < N) {
+            const int k = lane;
+            double x[NX], u[NU], xd[NX], fx[NX * NX], fu[NX * NU];
+#pragma unroll
+            for (int i = 0; i < NX; ++i) x[i] = sX[k * NX + i];
+#pragma unroll
+            for (int i = 0; i < NU; ++i) u[i] = sU[k * NU + i];
+            if (!p.is_linear) {
+#ifndef MMPC_DBG_NO_JAC
+                model_eval_jac<Model>(x, u, xd, fx, fu);
+#else
+                for (int i = 0; i < NX; ++i) { xd[i] = x[i] * u[0]; for (int q = 0; q < NX; ++q) fx[i*NX+q] = x[q]*x[i]; for (int q = 0; q < NU; ++q) fu[i*NU+q] = u[q]*x[i]; }
+#endif
+            } else {
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    double s = sLin[NX * NX + NX * NU + r];
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) {
+                        fx[r * NX + c] = sLin[r * NX + c];
+                        s = fma(fx[r * NX + c], x[c] - sX[c], s);
+                    }
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {
+                        fu[r * NU + c] = sLin[NX * NX + r * NU + c];
+                        s = fma(fu[r * NU + c], u[c] - up[c], s);
+                    }
+                    xd[r] = s;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                const double F = fma(hstep, xd[r], x[r]);
+                sF[k * NX + r] = F;
+                const double c = F - sX[(k + 1) * NX + r];
+                sC[k * NX + r] = c;
+                cmax = fmax(cmax, fabs(c));
+                nonfinite |= !isfinite(c);
+#pragma unroll
+                for (int q = 0; q < NX; ++q)
+                    sA[k * NX * NX + r * NX + q] = (r == q ? 1.0 : 0.0) + hstep * fx[r * NX + q];
+#pragma unroll
+                for (int q = 0; q < NU; ++q) sB[k * NX * NU + r * NU + q] = hstep * fu[r * NU + q];
+            }
+        }
+        __syncthreads();
+        cmax = wave_max(cmax);
+
+        const double Qa = sW[qa];
+        // ---- 2. forward d / e (all quads redundant, quad 0 stores) ----
+        {
+            double d = 0.0;  // d_0 = x0 - x_0 = 0 (x_0 is pinned)
+            for (int k = 0; k < N; ++k) {
+                const double* Ak = sA + k * NX * NX + qa * NX;
+                const double d0 = quad_bcast<0>(d), d1 = quad_bcast<1>(d), d2 = quad_bcast<2>(d),
+                             d3 = quad_bcast<3>(d);
+                const double ad = fma(Ak[0], d0, fma(Ak[1], d1, fma(Ak[2], d2, Ak[3] * d3)));
+                if (lane < NX) sE[k * NX + qa] = sF[k * NX + qa] + ad - sR[k * NX + qa];
+                d = ad + sC[k * NX + qa];
+            }
+        }
+        __syncthreads();
+
+        // ---- 3. adjoint lam and reduced gradient ----
+        double lmax;
+        {
+            double lam = Qa * sE[(N - 1) * NX + qa];
+            if (lane < NX) sLam[N * NX + qa] = lam;
+            lmax = fabs(lam);
+            for (int k = N - 1; k >= 1; --k) {
+                const double l0 = quad_bcast<0>(lam), l1 = quad_bcast<1>(lam), l2 = quad_bcast<2>(lam),
+                             l3 = quad_bcast<3>(lam);
+                const double* Ak = sA + k * NX * NX + qa;  // column qa of A_k
+                lam = fma(Qa, sE[(k - 1) * NX + qa],
+                          fma(Ak[0], l0, fma(Ak[NX], l1, fma(Ak[2 * NX], l2, Ak[3 * NX] * l3))));
+                if (lane < NX) sLam[k * NX + qa] = lam;
+                lmax = fmax(lmax, fabs(lam));
+            }
+        }
+        __syncthreads();
+        const int si = lane / NU, sr = lane - (lane / NU) * NU;  // Hessian row lane = (stage si, input sr)
+        const bool row_valid = lane < M;
+        double g = 0.0;
+        if (row_valid) {
+            const double* ln = sLam + (si + 1) * NX;
+#pragma unroll
+            for (int q = 0; q < NX; ++q) g = fma(sB[si * NX * NU + q * NU + sr], ln[q], g);
+            const double Rr = sW[NX + sr], Rmr = sW[NX + NU + sr];
+            const double ui = sU[si * NU + sr];
+            const double um = (si == 0) ? sUp[sr] : sU[(si - 1) * NU + sr];
+            g = fma(Rr, ui - um, fma(Rmr, ui, g));
+            if (si + 1 < N) g -= Rr * (sU[(si + 1) * NU + sr] - ui);
+            nonfinite |= !isfinite(g);
+        }
+        const double gmax = wave_max(fabs(2.0 * g));
+        kkt = fmax(gmax, cmax);
+        if (__any(nonfinite) || !isfinite(kkt)) {
+            status = ST_NONFINITE;
+            break;
+        }
+        if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
+            status = ST_CONVERGED;
+            break;
+        }
+        if (it == p.max_iter) {
+            status = ST_MAX_ITER;
+            break;
+        }
+
+        // ---- 4. Lyapunov recursion P, Z_i = B_i^T P_{i+1} (lanes 0..15) ----
+        {
+            const int pa = (lane >> 2) & 3, pb = lane & 3;
+            double P = (pa == pb) ? sW[pa] : 0.0;  // P_N = Q
+            for (int i = N - 1; i >= 0; --i) {
+                if (lane < 16) sP[lane] = P;
+                __syncthreads();
+                if (lane < 16) {
+                    const double* Ai = sA + i * NX * NX;
+                    const double* Bi = sB + i * NX * NU;
+                    if (pa < NU) {
+                        double z = 0.0;
+#pragma unroll
+                        for (int c = 0; c < NX; ++c) z = fma(Bi[c * NU + pa], sP[c * NX + pb], z);
+                        sZ[i * NU * NX + pa * NX + pb] = z;
+                    }
+                    double t = 0.0;
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) t = fma(sP[pa * NX + c], Ai[c * NX + pb], t);
+                    sT[lane] = t;
+                }
+                __syncthreads();
+                if (lane < 16) {
+                    const double* Ai = sA + i * NX * NX;
+                    double pn = (pa == pb) ? sW[pa] : 0.0;
+#pragma unroll
+                    for (int c = 0; c < NX; ++c) pn = fma(Ai[c * NX + pa], sT[c * NX + pb], pn);
+                    P = pn;
+                }
+            }
+        }
+        __syncthreads();
+
+        // ---- 5. condensed Hessian, one row per lane ----
+        double hrow[MMAX];
+#ifndef MMPC_DBG_NO_HBUILD
+        {
+            double z[NX], bcol[NX];
+#pragma unroll
+            for (int q = 0; q < NX; ++q) {
+                z[q] = row_valid ? sZ[si * NU * NX + sr * NX + q] : 0.0;
+                bcol[q] = row_valid ? sB[si * NX * NU + q * NU + sr] : 0.0;
+            }
+            // lower part, j <= si: t_(j) = Z_i Phi_{i+1,j+1}; t_(si) = z; t_(j) = t_(j+1) A_{j+1}
+            double t[NX] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = NMAX - 1; j >= 0; --j) {
+                if (j < NMAX - 1) {
+                    const double* A1 = sA + (j + 1) * NX * NX;
+                    double tn[NX];
+#pragma unroll
+                    for (int q = 0; q < NX; ++q)
+                        tn[q] = fma(t[0], A1[0 * NX + q],
+                                    fma(t[1], A1[1 * NX + q], fma(t[2], A1[2 * NX + q], t[3] * A1[3 * NX + q])));
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) t[q] = tn[q];
+                }
+                const bool at = (si == j);
+#pragma unroll
+                for (int q = 0; q < NX; ++q) t[q] = at ? z[q] : t[q];
+                const double* Bj = sB + j * NX * NU;
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    hrow[j * NU + c] = fma(t[0], Bj[0 * NU + c],
+                                           fma(t[1], Bj[1 * NU + c], fma(t[2], Bj[2 * NU + c], t[3] * Bj[3 * NU + c])));
+                    MMPC_PIN(hrow[j * NU + c]);
+                }
+#pragma unroll
+                for (int q = 0; q < NX; ++q) MMPC_PIN(t[q]);
+            }
+            // upper part, j > si: v_(j) = Phi_{j+1,i+1} B_i[:,r]; v_(si) = bcol; v_(j) = A_j v_(j-1)
+            double v[NX] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int j = 0; j < NMAX; ++j) {
+                const double* Aj = sA + j * NX * NX;
+                double vn[NX];
+#pragma unroll
+                for (int q = 0; q < NX; ++q)
+                    vn[q] = fma(Aj[q * NX + 0], v[0],
+                                fma(Aj[q * NX + 1], v[1], fma(Aj[q * NX + 2], v[2], Aj[q * NX + 3] * v[3])));
+                const bool at = (si == j);
+#pragma unroll
+                for (int q = 0; q < NX; ++q) v[q] = at ? bcol[q] : vn[q];
+                const double* Zj = sZ + j * NU * NX;
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const double hv = fma(Zj[c * NX + 0], v[0],
+                                          fma(Zj[c * NX + 1], v[1], fma(Zj[c * NX + 2], v[2], Zj[c * NX + 3] * v[3])));
+                    hrow[j * NU + c] = (j > si) ? hv : hrow[j * NU + c];
+                    MMPC_PIN(hrow[j * NU + c]);
+                }
+#pragma unroll
+                for (int q = 0; q < NX; ++q) MMPC_PIN(v[q]);
+            }
+            // D^T R D + Rm (ModelGenerator.cpp:216-221), padding rows/cols -> identity
+            const double Rr = sW[NX + (sr < NU ? sr : 0)], Rmr = sW[NX + NU + (sr < NU ? sr : 0)];
+            const double dterm = Rr * ((si + 1 < N) ? 2.0 : 1.0) + Rmr;
+#pragma unroll
+            for (int cidx = 0; cidx < MMAX; ++cidx) {
+                double hv = hrow[cidx];
+                hv += (cidx == lane) ? dterm : 0.0;
+                hv -= (cidx == lane - NU || cidx == lane + NU) ? Rr : 0.0;
+                if (cidx >= M) hv = 0.0;
+                if (!row_valid) hv = (cidx == lane) ? 1.0 : 0.0;
+                hrow[cidx] = hv;
+            }
+        }
+#else
+        for (int cidx = 0; cidx < MMAX; ++cidx) hrow[cidx] = (cidx == lane) ? 2.0 : sDU[cidx];
+#endif
+
+        // ---- 6. Gauss-Jordan on [H | -g] ----
+        double rhs = row_valid ? -g : 0.0;
+        double diag = 1.0;
+        bool fact_bad = false;
+#ifndef MMPC_DBG_NO_GJ
+        for (int k = 0; k < M; ++k) {
+            const double akk = readlane_d(hrow[0], k);
+            fact_bad |= !(akk > 0.0) || !isfinite(akk);
+            const double inv = rcp_nr(akk);
+            const double mlt = (lane == k) ? 0.0 : hrow[0] * inv;
+            diag = (lane == k) ? akk : diag;
+            rhs = fma(-mlt, readlane_d(rhs, k), rhs);
+            const int W1 = M - k - 1;  // columns left of the window after this step
+#pragma unroll
+            for (int j = 0; j < MMAX - 1; ++j) {
+                if ((j & 7) == 0 && j >= W1) break;
+                hrow[j] = fma(-mlt, readlane_d(hrow[j + 1], k), hrow[j + 1]);
+                MMPC_PIN(hrow[j]);
+            }
+        }
+#else
+        for (int j = 0; j < MMAX; ++j) rhs += hrow[j] * sDU[j];
+#endif
+        if (fact_bad) {
+            status = ST_FACT_FAILED;
+            break;
+        }
+        const double du = row_valid ? rhs / diag : 0.0;
+        if (row_valid) sDU[lane] = du;
+        __syncthreads();
+
+        // ---- 7. dx forward ----
+        {
+            double dx = 0.0;
+            if (lane < NX) sDX[qa] = 0.0;
+            for (int k = 0; k < N; ++k) {
+                const double* Ak = sA + k * NX * NX + qa * NX;
+                const double* Bk = sB + k * NX * NU + qa * NU;
+                const double x0v = quad_bcast<0>(dx), x1v = quad_bcast<1>(dx), x2v = quad_bcast<2>(dx),
+                             x3v = quad_bcast<3>(dx);
+                double dn = fma(Ak[0], x0v, fma(Ak[1], x1v, fma(Ak[2], x2v, fma(Ak[3], x3v, sC[k * NX + qa]))));
+#pragma unroll
+                for (int c = 0; c < NU; ++c) dn = fma(Bk[c], sDU[k * NU + c], dn);
+                if (lane < NX) sDX[(k + 1) * NX + qa] = dn;
+                dx = dn;
+            }
+        }
+        __syncthreads();
+
+        // ---- 8. l1-merit Armijo line search ----
+        mu = fmax(mu, 4.0 * wave_max(lmax) + 1.0);
+        double J0 = 0.0, c1 = 0.0, dJ = 0.0;
+        if (lane < N) {
+            const int k = lane;
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                const double er = sF[k * NX + r] - sR[k * NX + r];
+                const double qe = 2.0 * sW[r] * er;
+                J0 = fma(0.5 * qe, er, J0);
+                c1 += fabs(sC[k * NX + r]);
+                double ad = 0.0;
+#pragma unroll
+                for (int q = 0; q < NX; ++q) ad = fma(sA[k * NX * NX + r * NX + q], sDX[k * NX + q], ad);
+#pragma unroll
+                for (int q = 0; q < NU; ++q) ad = fma(sB[k * NX * NU + r * NU + q], sDU[k * NU + q], ad);
+                dJ = fma(qe, ad, dJ);
+            }
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                const double um = (k == 0) ? up[c] : sU[(k - 1) * NU + c];
+                const double dum = (k == 0) ? 0.0 : sDU[(k - 1) * NU + c];
+                const double uk = sU[k * NU + c], duk = sDU[k * NU + c];
+                const double dif = uk - um;
+                const double Rr = sW[NX + c], Rmr = sW[NX + NU + c];
+                J0 = fma(dif * Rr, dif, fma(uk * Rmr, uk, J0));
+                dJ = fma(2.0 * Rr * dif, duk - dum, fma(2.0 * Rmr * uk, duk, dJ));
+            }
+        }
+        J0 = wave_sum(J0);
+        c1 = wave_sum(c1);
+        dJ = wave_sum(dJ);
+        const double phi0 = fma(mu, c1, J0);
+        const double dphi = dJ - mu * c1;
+        double alpha = 1.0;
+        bool accepted = false;
+        for (int ls = 0; ls < 30; ++ls) {
+            double Jt = 0.0, ct = 0.0;
+            if (lane < N) {
+                const int k = lane;
+                double x[NX], u[NU], xd[NX];
+#pragma unroll
+                for (int i = 0; i < NX; ++i) x[i] = fma(alpha, sDX[k * NX + i], sX[k * NX + i]);
+#pragma unroll
+                for (int i = 0; i < NU; ++i) u[i] = fma(alpha, sDU[k * NU + i], sU[k * NU + i]);
+                if (!p.is_linear) {
+                    model_eval<Model>(x, u, xd);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        double s = sLin[NX * NX + NX * NU + r];
+#pragma unroll
+                        for (int c = 0; c < NX; ++c) s = fma(sLin[r * NX + c], x[c] - sX[c], s);
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) s = fma(sLin[NX * NX + r * NU + c], u[c] - up[c], s);
+                        xd[r] = s;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    const double F = fma(hstep, xd[r], x[r]);
+                    const double er = F - sR[k * NX + r];
+                    Jt = fma(er * sW[r], er, Jt);
+                    ct += fabs(F - fma(alpha, sDX[(k + 1) * NX + r], sX[(k + 1) * NX + r]));
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const double um = (k == 0) ? up[c] : fma(alpha, sDU[(k - 1) * NU + c], sU[(k - 1) * NU + c]);
+                    const double dif = u[c] - um;
+                    Jt = fma(dif * sW[NX + c], dif, fma(u[c] * sW[NX + NU + c], u[c], Jt));
+                }
+            }
+            Jt = wave_sum(Jt);
+            ct = wave_sum(ct);
+            const double phit = fma(mu, ct, Jt);
+            if (dphi >= -1e-14 * (1.0 + fabs(phi0)) || phit <= phi0 + 1e-4 * alpha * dphi) {
+                accepted = true;
+                break;
+            }
+            alpha *= 0.5;
+        }
+        if (!accepted) {
+            status = ST_LS_FAILED;
+            break;
+        }
+        for (int i = NX + lane; i < (N + 1) * NX; i += 64) sX[i] = fma(alpha, sDX[i], sX[i]);
+        if (lane < M) sU[lane] = fma(alpha, sDU[lane], sU[lane]);
+        __syncthreads();
+    }
+
+    // ---- bounds check (box constraints are reported, not yet enforced) ----
+    if (status == ST_CONVERGED && (p.u_lb || p.u_ub)) {
+        bool viol = false;
+        if (lane < M) {
+            const int r = lane % NU;
+            const double u = sU[lane];
+            if (p.u_lb) {
+                const double lb = p.u_lb[r];
+                viol |= (lb > -1e19) && (u < lb - 1e-9);
+            }
+            if (p.u_ub) {
+                const double ub = p.u_ub[r];
+                viol |= (ub < 1e19) && (u > ub + 1e-9);
+            }
+        }
+        if (__any(viol)) status = ST_BOUNDS;
+    }
+
+    // ---- write back V (reference layout) ----
+    __syncthreads();
+    double* Vout = p.V + inst * (int64_t)NV;
+    for (int i = lane; i < NV; i += 64) {
+        const int k = i / ND, r = i - k * ND;
+        double v;
+        if (k < N) v = (r < NX) ? sX[k * NX + r] : sU[k * NU + r - NX];
+        else v = sX[N * NX + r];
+        Vout[i] = v;
+    }
+    if (lane == 0) {
+        if (p.status) p.status[inst] = status;
+        if (p.iters) p.iters[inst] = it;
+        if (p.kkt) p.kkt[inst] = kkt;
+    }
+}
+
+}  // namespace mmpc

@@ -1,0 +1,259 @@
+"""Python binding of the mmpc C-ABI (include/mmpc.h) -- MI355X batched nonlinear MPC.
+
+This is a thin ctypes layer over ``lib/libmmpc.so``; every compute call runs the HIP
+kernels on the GPU.  There is no CPU fallback: if the library or a GPU is missing the
+calls raise ``MmpcError``.
+
+Reference mapping (mahi-mpc):
+  Solver(...)            ~ ModelControl::load_model      (src/Mahi/Mpc/ModelControl.cpp:21-73)
+  Solver.solve_batch*    ~ m_solver(m_solver_args)       (src/Mahi/Mpc/ModelControl.cpp:159), batched
+  Solver.linearize*      ~ <name>_get_A/_get_B/_get_x_dot_init externals (ModelGenerator.cpp:51-53)
+  write_model_json       ~ ModelGenerator::save_param_file (ModelGenerator.cpp:261-270)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import json
+import os
+import re
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG_DIR)                      # mahi-mpc_amd/
+REPO = os.path.dirname(ROOT)
+LIB_PATH = os.path.join(ROOT, "lib", "libmmpc.so")
+HEADER_PATH = os.path.join(REPO, "include", "mmpc.h")
+
+OK = 0
+STATUS = {0: "converged", 1: "max_iter", 2: "linesearch_failed", 3: "nonfinite",
+          4: "factorization_failed", 5: "bounds_violated"}
+STATUS_CONVERGED, STATUS_MAX_ITER, STATUS_LINESEARCH_FAILED = 0, 1, 2
+STATUS_NONFINITE, STATUS_FACTORIZATION_FAILED, STATUS_BOUNDS_VIOLATED = 3, 4, 5
+ERR = {-1: "invalid_arg", -2: "io", -3: "parse", -4: "unsupported", -5: "hip", -6: "no_device"}
+
+
+class MmpcError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"mmpc error {code} ({ERR.get(code, '?')}): {msg}")
+        self.code = code
+
+
+class Opts(C.Structure):
+    _fields_ = [("max_iter", C.c_int32), ("device", C.c_int32), ("tol_grad", C.c_double),
+                ("tol_defect", C.c_double)]
+
+
+class ModelInfo(C.Structure):
+    _fields_ = [("name", C.c_char * 128), ("model_id", C.c_int32), ("num_x", C.c_int32), ("num_u", C.c_int32),
+                ("num_shooting_nodes", C.c_int32), ("num_v", C.c_int32), ("num_g", C.c_int32),
+                ("is_linear", C.c_int32), ("step_size", C.c_double), ("timespan_us", C.c_int64),
+                ("step_size_us", C.c_int64), ("u_min", C.c_double * 16), ("u_max", C.c_double * 16),
+                ("x_min", C.c_double * 16), ("x_max", C.c_double * 16)]
+
+
+_lib = None
+_vp = C.c_void_p
+
+
+def build(force: bool = False) -> str:
+    """Compile lib/libmmpc.so for gfx950 with hipcc (make -C mahi-mpc_amd)."""
+    import subprocess
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", ROOT], check=True)
+    return LIB_PATH
+
+
+def header_functions(path: str = HEADER_PATH):
+    """Names of every function declared in include/mmpc.h."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(mmpc_\w+)\s*\(", text)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MmpcError(-2, f"{LIB_PATH} not built (run make -C mahi-mpc_amd)")
+        L = C.CDLL(LIB_PATH)
+        L.mmpc_abi_version.restype = C.c_int
+        L.mmpc_default_opts.argtypes = [C.POINTER(Opts)]
+        L.mmpc_create.argtypes = [C.c_char_p, C.POINTER(Opts), C.POINTER(_vp)]
+        L.mmpc_create_from_json.argtypes = [C.c_char_p, C.POINTER(Opts), C.POINTER(_vp)]
+        L.mmpc_destroy.argtypes = [_vp]
+        L.mmpc_get_model_info.argtypes = [_vp, C.POINTER(ModelInfo)]
+        L.mmpc_set_opts.argtypes = [_vp, C.POINTER(Opts)]
+        L.mmpc_solve_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 7
+        L.mmpc_solve_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 6
+        L.mmpc_linearize_batch.argtypes = [_vp, C.c_int64] + [_vp] * 6
+        L.mmpc_linearize_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 5
+        L.mmpc_nlp_eval_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 3
+        L.mmpc_synth_batch.argtypes = [_vp, C.c_uint64, C.c_int64, C.c_int64] + [_vp] * 4
+        L.mmpc_status_string.argtypes = [C.c_int32]
+        L.mmpc_status_string.restype = C.c_char_p
+        L.mmpc_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != OK:
+        raise MmpcError(rc, lib().mmpc_last_error().decode())
+
+
+def default_opts() -> Opts:
+    o = Opts()
+    lib().mmpc_default_opts(C.byref(o))
+    return o
+
+
+def write_model_json(path, name, num_x, num_u, step_size_us, num_shooting_nodes, is_linear=False,
+                     u_min=None, u_max=None, x_min=None, x_max=None, dll_filepath="", extra=None):
+    """Write <name>.json exactly as ModelGenerator::save_param_file does (ModelParameters.cpp:37-50),
+    including the +-10e30 defaults of the ModelParameters constructor (ModelParameters.cpp:14-24)."""
+    def dflt(v, n, s):
+        return list(v) if v is not None else [s * 10e30] * n
+    m = {"name": name, "timespan": int(step_size_us) * int(num_shooting_nodes), "step_size": int(step_size_us),
+         "num_x": num_x, "num_u": num_u, "num_shooting_nodes": num_shooting_nodes,
+         "x_min": dflt(x_min, num_x, -1), "u_min": dflt(u_min, num_u, -1),
+         "x_max": dflt(x_max, num_x, 1), "u_max": dflt(u_max, num_u, 1),
+         "dll_filepath": dll_filepath, "is_linear": bool(is_linear)}
+    if extra:
+        m.update(extra)
+    with open(path, "w") as fh:
+        json.dump({"model": m}, fh)
+    return path
+
+
+def _ptr(a):
+    """device/host pointer of a torch tensor, numpy array, int address or None."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    if hasattr(a, "data_ptr"):
+        return a.data_ptr()
+    if isinstance(a, np.ndarray):
+        assert a.flags.c_contiguous
+        return a.ctypes.data
+    raise TypeError(type(a))
+
+
+def _f64(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+class Solver:
+    """One loaded model (the reference's ModelControl without the thread/bookkeeping)."""
+
+    def __init__(self, model_json=None, json_text=None, max_iter=None, tol_grad=None, tol_defect=None,
+                 device=None):
+        o = default_opts()
+        if max_iter is not None:
+            o.max_iter = max_iter
+        if tol_grad is not None:
+            o.tol_grad = tol_grad
+        if tol_defect is not None:
+            o.tol_defect = tol_defect
+        if device is not None:
+            o.device = device
+        h = _vp()
+        if json_text is not None:
+            _check(lib().mmpc_create_from_json(json_text.encode(), C.byref(o), C.byref(h)))
+        else:
+            _check(lib().mmpc_create(os.fsencode(model_json), C.byref(o), C.byref(h)))
+        self._h = h
+        info = ModelInfo()
+        _check(lib().mmpc_get_model_info(h, C.byref(info)))
+        self.info = info
+        self.nx, self.nu, self.N = info.num_x, info.num_u, info.num_shooting_nodes
+        self.NV = info.num_v
+        self.h = info.step_size
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mmpc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- device-pointer API (torch tensors on the GPU or raw addresses) ----
+    def solve_batch(self, B, x0, u_prev, traj, weights, V, status=None, iters=None, kkt=None,
+                    weights_stride=0, u_lb=None, u_ub=None, stream=None):
+        _check(lib().mmpc_solve_batch(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights),
+                                      weights_stride, _ptr(u_lb), _ptr(u_ub), _ptr(V), _ptr(status),
+                                      _ptr(iters), _ptr(kkt), stream))
+
+    def synth(self, seed, first_index, B, x0, u_prev, traj, stream=None):
+        _check(lib().mmpc_synth_batch(self._h, seed, first_index, B, _ptr(x0), _ptr(u_prev), _ptr(traj), stream))
+
+    def nlp_eval(self, B, V, u_prev, traj, weights, J, defect_inf, weights_stride=0, stream=None):
+        _check(lib().mmpc_nlp_eval_batch(self._h, B, _ptr(V), _ptr(u_prev), _ptr(traj), _ptr(weights),
+                                         weights_stride, _ptr(J), _ptr(defect_inf), stream))
+
+    def linearize(self, B, x, u, A, Bm, xdot, stream=None):
+        _check(lib().mmpc_linearize_batch(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xdot), stream))
+
+    # ---- host (numpy) API, synchronous ----
+    def solve_batch_host(self, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None):
+        nx, nu, N, NV = self.nx, self.nu, self.N, self.NV
+        x0 = _f64(x0, (-1, nx))
+        B = x0.shape[0]
+        u_prev = _f64(u_prev, (B, nu))
+        traj = _f64(traj, (B, N, nx))
+        weights = _f64(weights)
+        ws = 0 if weights.ndim == 1 else weights.shape[-1]
+        V = np.zeros((B, NV)) if V is None else _f64(V, (B, NV)).copy()
+        st = np.zeros(B, np.int32)
+        it = np.zeros(B, np.int32)
+        kkt = np.zeros(B)
+        lb = None if u_lb is None else _f64(u_lb)
+        ub = None if u_ub is None else _f64(u_ub)
+        _check(lib().mmpc_solve_batch_host(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights), ws,
+                                           _ptr(lb), _ptr(ub), _ptr(V), _ptr(st), _ptr(it), _ptr(kkt)))
+        return dict(V=V, status=st, iters=it, kkt=kkt)
+
+    def linearize_host(self, x, u):
+        nx, nu = self.nx, self.nu
+        x = _f64(x, (-1, nx))
+        B = x.shape[0]
+        u = _f64(u, (B, nu))
+        A = np.zeros((B, nx * nx)); Bm = np.zeros((B, nx * nu)); xd = np.zeros((B, nx))
+        _check(lib().mmpc_linearize_batch_host(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xd)))
+        # column-major per instance (CasADi DM order) -> (B, nx, nx) row-major views
+        return (A.reshape(B, nx, nx).transpose(0, 2, 1), Bm.reshape(B, nu, nx).transpose(0, 2, 1), xd)
+
+
+def flops_per_iteration(N: int, nx: int = 4, nu: int = 2) -> dict:
+    """Algorithmic flop count of ONE SQP iteration of the HIP kernel (mul+add = 2), counted from
+    sqp_wave.h phase by phase (structure-exploiting: no flop on structural zeros).  See DESIGN.md."""
+    M = N * nu
+    f = {}
+    f["defect_recursion"] = N * (2 * nx * nx + 2 * nx)          # d_{k+1} = A d + c ; e
+    f["adjoint"] = (N - 1) * (2 * nx * nx + 2 * nx)             # lam recursion
+    f["gradient"] = M * (2 * nx + 8)
+    f["lyapunov"] = N * (4 * nx ** 3 + 2 * nu * nx * nx)        # P A, A^T (PA), Z = B^T P
+    # H rows: lower part sum over rows of (i+1) steps, upper part (N-1-i) steps; each step = vector x A
+    # (2 nx^2) plus nu outputs (2 nx each)
+    steps = sum((i + 1) + (N - 1 - i) for i in range(N)) * nu
+    f["hessian"] = steps * (2 * nx * nx + 2 * nu * nx)
+    f["gauss_jordan"] = sum(2 * (M - 1) * (M - k) for k in range(M)) + M  # rows x remaining cols, + rhs
+    f["dx_recursion"] = N * (2 * nx * nx + 2 * nu * nx + nx)
+    f["merit"] = N * (2 * nx * (nx + nu) + 12)
+    f["total"] = sum(f.values())
+    return f
+
+
+def survey_flops_per_iteration(N: int, nx: int = 4, nu: int = 2) -> int:
+    """SURVEY.md 8(d) reference count (explicit Gamma + block-triangular G^T Q G + Cholesky)."""
+    M, S = N * nu, N * nx
+    return int(N * (N - 1) / 2 * 2 * nx * nx * nu + N * (N + 1) * (N + 2) / 6 * 2 * nu * nu * nx
+               + M ** 3 / 3 + 4 * M * M + 2 * S * M + N * (nx * nx + nx * nu))

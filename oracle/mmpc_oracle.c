@@ -1,0 +1,546 @@
+/*
+ * mmpc_oracle.c -- CPU fp64 restatement of the mahi-mpc multiple-shooting NLP
+ * and of the Gauss-Newton SQP run by the HIP path.  TEST INFRASTRUCTURE ONLY
+ * (see mmpc_oracle.h).  Plain C99 + OpenMP, built by oracle/Makefile.
+ *
+ * What is restated, and from where (paths relative to the reference root):
+ *   dynamics      examples/ex_model_generate.cpp:24-43 (2-link arm, L=m=1, g=9.81)
+ *   Euler step    src/Mahi/Mpc/ModelGenerator.cpp:33-34     F(x,u) = x + h f(x,u)
+ *   F_lin         src/Mahi/Mpc/ModelGenerator.cpp:45-48
+ *   V layout      src/Mahi/Mpc/ModelGenerator.cpp:61-112    [x0,u0,x1,u1,...,x_{N-1},u_{N-1},xN]
+ *   p layout      src/Mahi/Mpc/ModelGenerator.cpp:129-187   [traj | Q | R | Rm | u_prev]
+ *   cost J        src/Mahi/Mpc/ModelGenerator.cpp:191-222   (no 1/2, error uses F(x_k,u_k))
+ *   defects g     src/Mahi/Mpc/ModelGenerator.cpp:206
+ *   x0 pinning    src/Mahi/Mpc/ModelControl.cpp:144-145
+ * The IPOPT call (ModelControl.cpp:159) is replaced by the GN-SQP described in
+ * DESIGN.md; this file implements it in the plain dense form (explicit Gamma,
+ * H = Gamma^T Q Gamma + D^T R D + Rm, textbook Cholesky) so that it shares no
+ * code or loop structure with the recursive condensing of the HIP kernel.
+ */
+#include "mmpc_oracle.h"
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NX 4
+#define NU 2
+#define ND (NX + NU)
+
+/* ---------------- forward-mode dual numbers (6 tangents: x then u) ---------------- */
+typedef struct { double v; double d[ND]; } dual;
+
+static dual dc(double c) { dual r; r.v = c; memset(r.d, 0, sizeof r.d); return r; }
+static dual dvar(double v, int i) { dual r = dc(v); r.d[i] = 1.0; return r; }
+static dual dadd(dual a, dual b) { dual r; r.v = a.v + b.v; for (int i = 0; i < ND; ++i) r.d[i] = a.d[i] + b.d[i]; return r; }
+static dual dsub(dual a, dual b) { dual r; r.v = a.v - b.v; for (int i = 0; i < ND; ++i) r.d[i] = a.d[i] - b.d[i]; return r; }
+static dual dmul(dual a, dual b) { dual r; r.v = a.v * b.v; for (int i = 0; i < ND; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i]; return r; }
+static dual dscale(double s, dual a) { dual r; r.v = s * a.v; for (int i = 0; i < ND; ++i) r.d[i] = s * a.d[i]; return r; }
+static dual ddiv(dual a, dual b) {
+    dual r; r.v = a.v / b.v;
+    for (int i = 0; i < ND; ++i) r.d[i] = (a.d[i] - r.v * b.d[i]) / b.v;
+    return r;
+}
+static dual dsin(dual a) { dual r; r.v = sin(a.v); double c = cos(a.v); for (int i = 0; i < ND; ++i) r.d[i] = c * a.d[i]; return r; }
+static dual dcos(dual a) { dual r; r.v = cos(a.v); double s = -sin(a.v); for (int i = 0; i < ND; ++i) r.d[i] = s * a.d[i]; return r; }
+static dual dneg(dual a) { return dscale(-1.0, a); }
+
+/* 2-link arm ODE right-hand side, restated from examples/ex_model_generate.cpp:36-37
+ * term by term (L = 1, m = 1, g = 9.81 at :24-26). */
+static void two_link_dual(const dual* x, const dual* u, dual* xd) {
+    const double L = 1.0, m = 1.0, g = 9.81;
+    dual qA = x[0], qB = x[1], dA = x[2], dB = x[3], TA = u[0], TB = u[1];
+    dual cB = dcos(qB), sB = dsin(qB), cA = dcos(qA), cAB = dcos(dadd(qA, qB));
+    const double LLm = L * L * m, Lgm = L * g * m;
+    dual dA2 = dmul(dA, dA), dB2 = dmul(dB, dB), dAdB = dmul(dA, dB), cBsB = dmul(cB, sB);
+    dual den = dscale(LLm, dsub(dmul(cB, cB), dc(2.0)));
+    /* qA_ddot numerator, :36 */
+    dual nA = dsub(TA, TB);
+    nA = dsub(nA, dmul(TB, cB));
+    nA = dadd(nA, dscale(LLm, dmul(dA2, sB)));
+    nA = dadd(nA, dscale(LLm, dmul(dB2, sB)));
+    nA = dsub(nA, dscale(2.0 * Lgm, cA));
+    nA = dadd(nA, dscale(LLm, dmul(dA2, cBsB)));
+    nA = dadd(nA, dscale(2.0 * LLm, dmul(dAdB, sB)));
+    nA = dadd(nA, dscale(Lgm, dmul(cAB, cB)));
+    /* qB_ddot numerator, :37 */
+    dual nB = dsub(dadd(TA, dc(0.0)), dscale(3.0, TB));
+    nB = dadd(nB, dmul(TA, cB));
+    nB = dsub(nB, dscale(2.0, dmul(TB, cB)));
+    nB = dadd(nB, dscale(2.0 * Lgm, cAB));
+    nB = dadd(nB, dscale(3.0 * LLm, dmul(dA2, sB)));
+    nB = dadd(nB, dscale(LLm, dmul(dB2, sB)));
+    nB = dsub(nB, dscale(2.0 * Lgm, cA));
+    nB = dadd(nB, dscale(2.0 * LLm, dmul(dA2, cBsB)));
+    nB = dadd(nB, dscale(LLm, dmul(dB2, cBsB)));
+    nB = dsub(nB, dscale(2.0 * Lgm, dmul(cA, cB)));
+    nB = dadd(nB, dscale(2.0 * LLm, dmul(dAdB, sB)));
+    nB = dadd(nB, dscale(Lgm, dmul(cAB, cB)));
+    nB = dadd(nB, dscale(2.0 * LLm, dmul(dAdB, cBsB)));
+    xd[0] = dA;
+    xd[1] = dB;
+    xd[2] = dneg(ddiv(nA, den));
+    xd[3] = ddiv(nB, den);
+}
+
+void oracle_two_link_jac(const double* x, const double* u, double* A, double* B, double* xdot) {
+    dual xv[NX], uv[NU], xd[NX];
+    for (int i = 0; i < NX; ++i) xv[i] = dvar(x[i], i);
+    for (int i = 0; i < NU; ++i) uv[i] = dvar(u[i], NX + i);
+    two_link_dual(xv, uv, xd);
+    for (int r = 0; r < NX; ++r) {
+        if (xdot) xdot[r] = xd[r].v;
+        if (A) for (int c = 0; c < NX; ++c) A[r * NX + c] = xd[r].d[c];
+        if (B) for (int c = 0; c < NU; ++c) B[r * NU + c] = xd[r].d[NX + c];
+    }
+}
+
+void oracle_two_link_xdot(const double* x, const double* u, double* xdot) {
+    oracle_two_link_jac(x, u, NULL, NULL, xdot);
+}
+
+void oracle_f_lin(int nx, int nu, double h, const double* A, const double* B, const double* x,
+                  const double* u, const double* xdot_init, const double* x_init,
+                  const double* u_init, double* x_next) {
+    /* x_next = x + h (A (x - x*) + B (u - u*) + xdot*)   ModelGenerator.cpp:47-48 */
+    for (int r = 0; r < nx; ++r) {
+        double s = xdot_init[r];
+        for (int c = 0; c < nx; ++c) s += A[r * nx + c] * (x[c] - x_init[c]);
+        for (int c = 0; c < nu; ++c) s += B[r * nu + c] * (u[c] - u_init[c]);
+        x_next[r] = x[r] + h * s;
+    }
+}
+
+/* ---------------- NLP pieces ---------------- */
+/* linear mode (ModelGenerator.cpp:137-187, ModelControl.cpp:125-136): when non-NULL, lin holds
+ * A* (row-major), B*, xdot*, x*, u* and the dynamics are F_lin instead of F. */
+static _Thread_local const double* g_lin = NULL;
+
+static void stage_jac(const double* x, const double* u, double* A, double* Bc, double* xd) {
+    if (!g_lin) {
+        oracle_two_link_jac(x, u, A, Bc, xd);
+        return;
+    }
+    const double *As = g_lin, *Bs = g_lin + NX * NX, *fs = Bs + NX * NU, *xs = fs + NX, *us = xs + NX;
+    for (int r = 0; r < NX; ++r) {
+        double s = fs[r];
+        for (int c = 0; c < NX; ++c) { A[r * NX + c] = As[r * NX + c]; s += As[r * NX + c] * (x[c] - xs[c]); }
+        for (int c = 0; c < NU; ++c) { Bc[r * NU + c] = Bs[r * NU + c]; s += Bs[r * NU + c] * (u[c] - us[c]); }
+        xd[r] = s;
+    }
+}
+
+static void euler_step(double h, const double* x, const double* u, double* F, double* Ad, double* Bd) {
+    double A[NX * NX], Bc[NX * NU], xd[NX];
+    stage_jac(x, u, A, Bc, xd);
+    for (int r = 0; r < NX; ++r) {
+        F[r] = x[r] + h * xd[r];
+        if (Ad) for (int c = 0; c < NX; ++c) Ad[r * NX + c] = (r == c ? 1.0 : 0.0) + h * A[r * NX + c];
+        if (Bd) for (int c = 0; c < NU; ++c) Bd[r * NU + c] = h * Bc[r * NU + c];
+    }
+}
+
+/* J and defects of ModelGenerator.cpp:191-222 at the packed V */
+void oracle_nlp_eval(int model, int N, double h, const double* V, const double* u_prev,
+                     const double* traj, const double* w, double* Jout, double* g) {
+    (void)model;  /* nonlinear model; in linear mode solve_one evaluates with g_lin set */
+    const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
+    double J = 0.0;
+    for (int k = 0; k < N; ++k) {
+        const double* xk = V + k * ND;
+        const double* uk = xk + NX;
+        const double* xk1 = V + (k + 1) * ND;
+        const double* ukm = (k == 0) ? u_prev : V + (k - 1) * ND + NX;
+        double F[NX];
+        euler_step(h, xk, uk, F, NULL, NULL);
+        for (int r = 0; r < NX; ++r) {
+            if (g) g[k * NX + r] = F[r] - xk1[r];
+            double e = F[r] - traj[k * NX + r];
+            J += e * Q[r] * e;
+        }
+        for (int c = 0; c < NU; ++c) {
+            double du = uk[c] - ukm[c];
+            J += du * R[c] * du + uk[c] * Rm[c] * uk[c];
+        }
+    }
+    if (Jout) *Jout = J;
+}
+
+void oracle_reduced_gradient(int model, int N, double h, const double* x0, const double* U,
+                             const double* u_prev, const double* traj, const double* w,
+                             double* grad) {
+    (void)model;
+    const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
+    double* X = (double*)malloc(sizeof(double) * (N + 1) * NX);
+    double* Ad = (double*)malloc(sizeof(double) * N * NX * NX);
+    double* Bd = (double*)malloc(sizeof(double) * N * NX * NU);
+    memcpy(X, x0, sizeof(double) * NX);
+    for (int k = 0; k < N; ++k) euler_step(h, X + k * NX, U + k * NU, X + (k + 1) * NX, Ad + k * NX * NX, Bd + k * NX * NU);
+    /* adjoint: lam_{k} = 2Q(x_{k} - r_{k-1}) + A_k^T lam_{k+1}, lam_N = 2Q(x_N - r_{N-1}) */
+    double lam[NX], tmp[NX];
+    for (int r = 0; r < NX; ++r) lam[r] = 2.0 * Q[r] * (X[N * NX + r] - traj[(N - 1) * NX + r]);
+    for (int k = N - 1; k >= 0; --k) {
+        /* grad wrt u_k: B_k^T lam_{k+1} */
+        for (int c = 0; c < NU; ++c) {
+            double s = 0.0;
+            for (int r = 0; r < NX; ++r) s += Bd[k * NX * NU + r * NU + c] * lam[r];
+            double ukm = (k == 0) ? u_prev[c] : U[(k - 1) * NU + c];
+            s += 2.0 * R[c] * (U[k * NU + c] - ukm) + 2.0 * Rm[c] * U[k * NU + c];
+            if (k + 1 < N) s -= 2.0 * R[c] * (U[(k + 1) * NU + c] - U[k * NU + c]);
+            grad[k * NU + c] = s;
+        }
+        if (k == 0) break;
+        for (int c = 0; c < NX; ++c) {
+            double s = 0.0;
+            for (int r = 0; r < NX; ++r) s += Ad[k * NX * NX + r * NX + c] * lam[r];
+            tmp[c] = s + 2.0 * Q[c] * (X[k * NX + c] - traj[(k - 1) * NX + c]);
+        }
+        memcpy(lam, tmp, sizeof lam);
+    }
+    free(X); free(Ad); free(Bd);
+}
+
+/* ---------------- dense GN-SQP for one instance ---------------- */
+typedef struct {
+    int N, M;
+    double *X, *U, *F, *Ad, *Bd, *c, *d, *e, *G, *H, *g, *du, *dx, *lam, *Xt, *Ut, *Ft;
+} ws_t;
+
+static void ws_alloc(ws_t* s, int N) {
+    s->N = N; s->M = N * NU;
+    size_t M = (size_t)s->M;
+    s->X = calloc((size_t)(N + 1) * NX, sizeof(double));
+    s->U = calloc((size_t)N * NU, sizeof(double));
+    s->F = calloc((size_t)N * NX, sizeof(double));
+    s->Ad = calloc((size_t)N * NX * NX, sizeof(double));
+    s->Bd = calloc((size_t)N * NX * NU, sizeof(double));
+    s->c = calloc((size_t)N * NX, sizeof(double));
+    s->d = calloc((size_t)(N + 1) * NX, sizeof(double));
+    s->e = calloc((size_t)N * NX, sizeof(double));
+    s->G = calloc((size_t)N * NX * M, sizeof(double));
+    s->H = calloc(M * M, sizeof(double));
+    s->g = calloc(M, sizeof(double));
+    s->du = calloc(M, sizeof(double));
+    s->dx = calloc((size_t)(N + 1) * NX, sizeof(double));
+    s->lam = calloc((size_t)(N + 1) * NX, sizeof(double));
+    s->Xt = calloc((size_t)(N + 1) * NX, sizeof(double));
+    s->Ut = calloc((size_t)N * NU, sizeof(double));
+    s->Ft = calloc((size_t)N * NX, sizeof(double));
+}
+static void ws_free(ws_t* s) {
+    free(s->X); free(s->U); free(s->F); free(s->Ad); free(s->Bd); free(s->c); free(s->d);
+    free(s->e); free(s->G); free(s->H); free(s->g); free(s->du); free(s->dx); free(s->lam);
+    free(s->Xt); free(s->Ut); free(s->Ft);
+}
+
+/* merit pieces at (X,U): J and sum |c| (F returned) */
+static void merit_eval(int N, double h, const double* X, const double* U, const double* u_prev,
+                       const double* traj, const double* w, double* F, double* J, double* c1) {
+    const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
+    double Jv = 0.0, cs = 0.0;
+    for (int k = 0; k < N; ++k) {
+        euler_step(h, X + k * NX, U + k * NU, F + k * NX, NULL, NULL);
+        for (int r = 0; r < NX; ++r) {
+            double e = F[k * NX + r] - traj[k * NX + r];
+            Jv += e * Q[r] * e;
+            cs += fabs(F[k * NX + r] - X[(k + 1) * NX + r]);
+        }
+        for (int q = 0; q < NU; ++q) {
+            double um = (k == 0) ? u_prev[q] : U[(k - 1) * NU + q];
+            double du = U[k * NU + q] - um;
+            Jv += du * R[q] * du + U[k * NU + q] * Rm[q] * U[k * NU + q];
+        }
+    }
+    *J = Jv; *c1 = cs;
+}
+
+static int chol_solve(int M, double* H, double* b /* in: rhs, out: solution */) {
+    for (int j = 0; j < M; ++j) {
+        double s = H[j * M + j];
+        for (int k = 0; k < j; ++k) s -= H[j * M + k] * H[j * M + k];
+        if (!(s > 0.0) || !isfinite(s)) return -1;
+        double Ljj = sqrt(s);
+        H[j * M + j] = Ljj;
+        for (int i = j + 1; i < M; ++i) {
+            double t = H[i * M + j];
+            for (int k = 0; k < j; ++k) t -= H[i * M + k] * H[j * M + k];
+            H[i * M + j] = t / Ljj;
+        }
+    }
+    for (int i = 0; i < M; ++i) {
+        double t = b[i];
+        for (int k = 0; k < i; ++k) t -= H[i * M + k] * b[k];
+        b[i] = t / H[i * M + i];
+    }
+    for (int i = M - 1; i >= 0; --i) {
+        double t = b[i];
+        for (int k = i + 1; k < M; ++k) t -= H[k * M + i] * b[k];
+        b[i] = t / H[i * M + i];
+    }
+    return 0;
+}
+
+static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, const double* traj,
+                     const double* w, const double* u_lb, const double* u_ub, int max_iter,
+                     double tol_grad, double tol_defect, double* V, int32_t* iters_out,
+                     double* kkt_out, double* J_out) {
+    const int N = s->N, M = s->M;
+    const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
+    /* unpack V (ModelGenerator.cpp:86-112); x_0 pinned to the measured state */
+    for (int k = 0; k < N; ++k) {
+        memcpy(s->X + k * NX, V + k * ND, sizeof(double) * NX);
+        memcpy(s->U + k * NU, V + k * ND + NX, sizeof(double) * NU);
+    }
+    memcpy(s->X + N * NX, V + N * ND, sizeof(double) * NX);
+    memcpy(s->X, x0, sizeof(double) * NX);
+
+    int status = ORACLE_MAX_ITER, it = 0;
+    double kkt = INFINITY, mu = 0.0;
+    for (it = 0; it <= max_iter; ++it) {
+        /* (1) stage evaluation: F_k, A_k = I + h df/dx, B_k = h df/du */
+        for (int k = 0; k < N; ++k)
+            euler_step(h, s->X + k * NX, s->U + k * NU, s->F + k * NX, s->Ad + k * NX * NX, s->Bd + k * NX * NU);
+        double cmax = 0.0;
+        for (int i = 0; i < N * NX; ++i) {
+            s->c[i] = s->F[i] - s->X[NX + i];
+            if (fabs(s->c[i]) > cmax || s->c[i] != s->c[i]) cmax = fabs(s->c[i]);
+        }
+        /* (2) d_0 = 0, d_{k+1} = A_k d_k + c_k ; e_k = F_k + A_k d_k - r_k */
+        memset(s->d, 0, sizeof(double) * NX);
+        for (int k = 0; k < N; ++k) {
+            for (int r = 0; r < NX; ++r) {
+                double ad = 0.0;
+                for (int q = 0; q < NX; ++q) ad += s->Ad[k * NX * NX + r * NX + q] * s->d[k * NX + q];
+                s->d[(k + 1) * NX + r] = ad + s->c[k * NX + r];
+                s->e[k * NX + r] = s->F[k * NX + r] + ad - traj[k * NX + r];
+            }
+        }
+        /* (3) dense Gamma: rows = x_{k+1} (k<N), cols = u_j (j<=k) */
+        memset(s->G, 0, sizeof(double) * (size_t)N * NX * M);
+        for (int j = 0; j < N; ++j) {
+            double col[NX][NU], nxt[NX][NU];
+            for (int r = 0; r < NX; ++r) for (int q = 0; q < NU; ++q) col[r][q] = s->Bd[j * NX * NU + r * NU + q];
+            for (int k = j; k < N; ++k) {
+                if (k > j) {
+                    for (int r = 0; r < NX; ++r) for (int q = 0; q < NU; ++q) {
+                        double t = 0.0;
+                        for (int p = 0; p < NX; ++p) t += s->Ad[k * NX * NX + r * NX + p] * col[p][q];
+                        nxt[r][q] = t;
+                    }
+                    memcpy(col, nxt, sizeof col);
+                }
+                for (int r = 0; r < NX; ++r) for (int q = 0; q < NU; ++q)
+                    s->G[(size_t)(k * NX + r) * M + j * NU + q] = col[r][q];
+            }
+        }
+        /* (4) H = G^T Qb G + D^T Rb D + Rmb ; g = G^T Qb e + D^T Rb (D u - u~) + Rmb u */
+        for (int a = 0; a < M; ++a) {
+            for (int b = 0; b <= a; ++b) {
+                double t = 0.0;
+                for (int i = 0; i < N * NX; ++i) t += s->G[(size_t)i * M + a] * Q[i % NX] * s->G[(size_t)i * M + b];
+                s->H[a * M + b] = t;
+                s->H[b * M + a] = t;
+            }
+            double t = 0.0;
+            for (int i = 0; i < N * NX; ++i) t += s->G[(size_t)i * M + a] * Q[i % NX] * s->e[i];
+            s->g[a] = t;
+        }
+        for (int k = 0; k < N; ++k) {
+            for (int q = 0; q < NU; ++q) {
+                int a = k * NU + q;
+                double um = (k == 0) ? u_prev[q] : s->U[(k - 1) * NU + q];
+                s->H[a * M + a] += R[q] + Rm[q];
+                s->g[a] += R[q] * (s->U[a] - um) + Rm[q] * s->U[a];
+                if (k + 1 < N) {
+                    s->H[a * M + a] += R[q];
+                    s->H[a * M + a + NU] -= R[q];
+                    s->H[(a + NU) * M + a] -= R[q];
+                    s->g[a] -= R[q] * (s->U[a + NU] - s->U[a]);
+                }
+            }
+        }
+        double gmax = 0.0;
+        for (int a = 0; a < M; ++a) { double t = fabs(2.0 * s->g[a]); if (t > gmax || t != t) gmax = t; }
+        kkt = gmax > cmax ? gmax : cmax;
+        if (!isfinite(kkt)) { status = ORACLE_NONFINITE; break; }
+        if (gmax <= tol_grad && cmax <= tol_defect) { status = ORACLE_CONVERGED; break; }
+        if (it == max_iter) { status = ORACLE_MAX_ITER; break; }
+
+        /* (5) adjoint for the penalty weight: lam_N = Q e_{N-1}; lam_k = Q e_{k-1} + A_k^T lam_{k+1} */
+        for (int r = 0; r < NX; ++r) s->lam[N * NX + r] = Q[r] * s->e[(N - 1) * NX + r];
+        double lmax = 0.0;
+        for (int r = 0; r < NX; ++r) if (fabs(s->lam[N * NX + r]) > lmax) lmax = fabs(s->lam[N * NX + r]);
+        for (int k = N - 1; k >= 1; --k) {
+            for (int r = 0; r < NX; ++r) {
+                double t = Q[r] * s->e[(k - 1) * NX + r];
+                for (int p = 0; p < NX; ++p) t += s->Ad[k * NX * NX + p * NX + r] * s->lam[(k + 1) * NX + p];
+                s->lam[k * NX + r] = t;
+                if (fabs(t) > lmax) lmax = fabs(t);
+            }
+        }
+
+        /* (6) step: Cholesky of H, du = -H^-1 g; dx_0 = 0, dx_{k+1} = A dx + B du + c */
+        for (int a = 0; a < M; ++a) s->du[a] = -s->g[a];
+        if (chol_solve(M, s->H, s->du) != 0) { status = ORACLE_FACTORIZATION_FAILED; break; }
+        memset(s->dx, 0, sizeof(double) * NX);
+        for (int k = 0; k < N; ++k)
+            for (int r = 0; r < NX; ++r) {
+                double t = s->c[k * NX + r];
+                for (int q = 0; q < NX; ++q) t += s->Ad[k * NX * NX + r * NX + q] * s->dx[k * NX + q];
+                for (int q = 0; q < NU; ++q) t += s->Bd[k * NX * NU + r * NU + q] * s->du[k * NU + q];
+                s->dx[(k + 1) * NX + r] = t;
+            }
+
+        /* (7) l1-merit Armijo backtracking: phi = J + mu sum|c| */
+        double mu_new = 4.0 * lmax + 1.0;
+        if (mu_new > mu) mu = mu_new;
+        double J0 = 0.0, c1 = 0.0, dJ = 0.0;
+        for (int k = 0; k < N; ++k) {
+            double qe[NX];
+            for (int r = 0; r < NX; ++r) {
+                qe[r] = 2.0 * Q[r] * (s->F[k * NX + r] - traj[k * NX + r]);
+                J0 += 0.5 * qe[r] * (s->F[k * NX + r] - traj[k * NX + r]);
+                c1 += fabs(s->c[k * NX + r]);
+            }
+            for (int r = 0; r < NX; ++r) {
+                double ax = 0.0, bu = 0.0;
+                for (int q = 0; q < NX; ++q) ax += s->Ad[k * NX * NX + r * NX + q] * s->dx[k * NX + q];
+                for (int q = 0; q < NU; ++q) bu += s->Bd[k * NX * NU + r * NU + q] * s->du[k * NU + q];
+                dJ += qe[r] * (ax + bu);
+            }
+            for (int q = 0; q < NU; ++q) {
+                double um = (k == 0) ? u_prev[q] : s->U[(k - 1) * NU + q];
+                double dum = (k == 0) ? 0.0 : s->du[(k - 1) * NU + q];
+                double dif = s->U[k * NU + q] - um;
+                J0 += dif * R[q] * dif + s->U[k * NU + q] * Rm[q] * s->U[k * NU + q];
+                dJ += 2.0 * R[q] * dif * (s->du[k * NU + q] - dum) + 2.0 * Rm[q] * s->U[k * NU + q] * s->du[k * NU + q];
+            }
+        }
+        double phi0 = J0 + mu * c1;
+        double dphi = dJ - mu * c1;
+        double alpha = 1.0;
+        int accepted = 0;
+        for (int ls = 0; ls < 30; ++ls) {
+            for (int i = 0; i < (N + 1) * NX; ++i) s->Xt[i] = s->X[i] + alpha * s->dx[i];
+            for (int i = 0; i < M; ++i) s->Ut[i] = s->U[i] + alpha * s->du[i];
+            double Jt, ct;
+            merit_eval(N, h, s->Xt, s->Ut, u_prev, traj, w, s->Ft, &Jt, &ct);
+            double phit = Jt + mu * ct;
+            if (dphi >= -1e-14 * (1.0 + fabs(phi0)) || phit <= phi0 + 1e-4 * alpha * dphi) { accepted = 1; break; }
+            alpha *= 0.5;
+        }
+        if (!accepted) { status = ORACLE_LINESEARCH_FAILED; break; }
+        memcpy(s->X, s->Xt, sizeof(double) * (N + 1) * NX);
+        memcpy(s->U, s->Ut, sizeof(double) * M);
+    }
+    /* pack V */
+    for (int k = 0; k < N; ++k) {
+        memcpy(V + k * ND, s->X + k * NX, sizeof(double) * NX);
+        memcpy(V + k * ND + NX, s->U + k * NU, sizeof(double) * NU);
+    }
+    memcpy(V + N * ND, s->X + N * NX, sizeof(double) * NX);
+    if (status == ORACLE_CONVERGED && (u_lb || u_ub)) {
+        for (int k = 0; k < N; ++k)
+            for (int q = 0; q < NU; ++q) {
+                double u = s->U[k * NU + q];
+                if ((u_lb && u_lb[q] > -1e19 && u < u_lb[q] - 1e-9) || (u_ub && u_ub[q] < 1e19 && u > u_ub[q] + 1e-9))
+                    status = ORACLE_BOUNDS_VIOLATED;
+            }
+    }
+    if (J_out) {
+        double J;
+        oracle_nlp_eval(0, N, h, V, u_prev, traj, w, &J, NULL);
+        *J_out = J;
+    }
+    *iters_out = it;
+    *kkt_out = kkt;
+    return status;
+}
+
+int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, const double* x0,
+                       const double* u_prev, const double* traj, const double* weights,
+                       int64_t w_stride, const double* u_lb, const double* u_ub, int max_iter,
+                       double tol_grad, double tol_defect, double* V, int32_t* status,
+                       int32_t* iters, double* kkt, double* Jout, int nthreads) {
+    if (model != ORACLE_MODEL_TWO_LINK_ARM || N < 1 || B < 0) return -1;
+    const int NV = NX * (N + 1) + NU * N;
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+#pragma omp parallel
+    {
+        ws_t s;
+        ws_alloc(&s, N);
+#pragma omp for schedule(dynamic, 4)
+        for (int64_t b = 0; b < B; ++b) {
+            int32_t it;
+            double kk, J;
+            double lin[NX * NX + NX * NU + 3 * NX];
+            if (is_linear) {
+                /* A*, B*, xdot* at (state, control) = (x0, u_prev), ModelControl.cpp:125-136 */
+                oracle_two_link_jac(x0 + b * NX, u_prev + b * NU, lin, lin + NX * NX, lin + NX * NX + NX * NU);
+                memcpy(lin + NX * NX + NX * NU + NX, x0 + b * NX, sizeof(double) * NX);
+                memcpy(lin + NX * NX + NX * NU + 2 * NX, u_prev + b * NU, sizeof(double) * NU);
+                g_lin = lin;
+            } else {
+                g_lin = NULL;
+            }
+            status[b] = solve_one(&s, h, x0 + b * NX, u_prev + b * NU, traj + b * (int64_t)N * NX,
+                                  weights + b * w_stride, u_lb, u_ub, max_iter, tol_grad, tol_defect,
+                                  V + b * NV, &it, &kk, &J);
+            iters[b] = it;
+            kkt[b] = kk;
+            if (Jout) Jout[b] = J;
+            g_lin = NULL;
+        }
+        ws_free(&s);
+    }
+    return 0;
+}
+
+/* ---------------- synthetic instances (cfg#2) ---------------- */
+static uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+static double unit_draw(uint64_t seed, int64_t index, int j) {
+    uint64_t v = splitmix64(seed ^ splitmix64((uint64_t)index * 16ull + (uint64_t)j));
+    return (double)(v >> 11) * 0x1.0p-53;
+}
+
+/* lo + span * u with the product rounded separately (never fused), so that the C, HIP and Python
+ * generators produce bit-identical instances. */
+__attribute__((optimize("-ffp-contract=off"))) static double affine_draw(double lo, double span, double u) {
+    volatile double p = span * u;
+    return lo + p;
+}
+
+__attribute__((optimize("-ffp-contract=off")))
+void oracle_synth_two_link(uint64_t seed, int64_t first, int64_t B, int N, double h,
+                           double* x0, double* u_prev, double* traj) {
+    const double PI = 3.14159265358979323846;
+    for (int64_t b = 0; b < B; ++b) {
+        int64_t gi = first + b;
+        x0[b * 4 + 0] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 0));
+        x0[b * 4 + 1] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 1));
+        x0[b * 4 + 2] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 2));
+        x0[b * 4 + 3] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 3));
+        u_prev[b * 2 + 0] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 4));
+        u_prev[b * 2 + 1] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 5));
+        double a = affine_draw(0.5, 0.5, unit_draw(seed, gi, 6));
+        double f = affine_draw(0.25, 0.75, unit_draw(seed, gi, 7));
+        double ph = affine_draw(0.0, 2.0 * PI, unit_draw(seed, gi, 8));
+        for (int k = 0; k < N; ++k) {
+            double arg = 2.0 * PI * f * (k * h) + ph;
+            double sv = a * sin(arg), cv = 2.0 * PI * f * a * cos(arg);
+            double* r = traj + (b * N + k) * 4;
+            r[0] = sv; r[1] = -sv; r[2] = cv; r[3] = -cv;
+        }
+    }
+}

@@ -1,0 +1,75 @@
+/*
+ * mmpc_oracle.h -- CPU fp64 restatement of the mahi-mpc NLP and of the
+ * Gauss-Newton SQP that the HIP path runs.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the
+ * checker / CPU baseline.  The product path (mahi-mpc_amd/) never links it.
+ *
+ * Parity status: the reference solve (CasADi @ fadc864 + IPOPT 3.14.3) cannot
+ * be built or run here, so the full solve is pinned by
+ *   - the reference's own known-answer material (lin_test.m:31-50, lin_test.m:22-28,
+ *     old/Models/DoublePendulumModel.hpp closed-form Jacobian, src/nlp_codegen.cpp:41-62)
+ *     restated as fixtures in tests/golden/, and
+ *   - independent scipy solves of the identical NLP (tests/golden/make_golden.py).
+ * See DESIGN.md "Oracle".
+ */
+#ifndef MMPC_ORACLE_H
+#define MMPC_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORACLE_MODEL_TWO_LINK_ARM = 0 };
+
+/* per-instance status, same numbering as include/mmpc.h */
+enum {
+    ORACLE_CONVERGED = 0,
+    ORACLE_MAX_ITER = 1,
+    ORACLE_LINESEARCH_FAILED = 2,
+    ORACLE_NONFINITE = 3,
+    ORACLE_FACTORIZATION_FAILED = 4,
+    ORACLE_BOUNDS_VIOLATED = 5
+};
+
+/* x_dot = f(x,u) of the 2-link arm, examples/ex_model_generate.cpp:24-43 */
+void oracle_two_link_xdot(const double* x, const double* u, double* xdot);
+/* continuous Jacobians A = df/dx (4x4), B = df/du (4x2), ROW-major, plus xdot */
+void oracle_two_link_jac(const double* x, const double* u, double* A, double* B, double* xdot);
+/* linearised Euler step F_lin, ModelGenerator.cpp:47-48 (A,B row-major here) */
+void oracle_f_lin(int nx, int nu, double h, const double* A, const double* B, const double* x,
+                  const double* u, const double* xdot_init, const double* x_init,
+                  const double* u_init, double* x_next);
+
+/* NLP value: J (ModelGenerator.cpp:208-222) and defects g (ModelGenerator.cpp:206)
+ * at the decision vector V (layout ModelGenerator.cpp:61-112). */
+void oracle_nlp_eval(int model, int N, double h, const double* V, const double* u_prev,
+                     const double* traj, const double* weights, double* J, double* g);
+/* gradient of the single-shooting objective w.r.t. U (x rolled out from x0),
+ * exact via the adjoint; used as an independent stationarity certificate. */
+void oracle_reduced_gradient(int model, int N, double h, const double* x0, const double* U,
+                             const double* u_prev, const double* traj, const double* weights,
+                             double* grad);
+
+/* Batched GN-SQP solve (the algorithm of DESIGN.md "Solver"), OpenMP over instances.
+ * Layouts are instance-major:  x0[B][nx], u_prev[B][nu], traj[B][N*nx],
+ * weights[w_stride==0 ? 1 : B][nx+2nu] = (Q | R | Rm), V[B][NV] (warm start in,
+ * solution out; V[b][0:nx] is overwritten by x0 as the reference pins x_0 by
+ * bounds, ModelControl.cpp:144-145).  u_lb/u_ub may be NULL (unbounded).  is_linear selects
+ * F_lin with A*, B*, xdot* taken at (x0, u_prev) (ModelControl.cpp:125-136). */
+int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, const double* x0,
+                       const double* u_prev, const double* traj, const double* weights,
+                       int64_t w_stride, const double* u_lb, const double* u_ub, int max_iter,
+                       double tol_grad, double tol_defect, double* V, int32_t* status,
+                       int32_t* iters, double* kkt, double* Jout, int nthreads);
+
+/* counter-based synthetic cfg#2 instances: splitmix64(seed, index) */
+void oracle_synth_two_link(uint64_t seed, int64_t first_index, int64_t B, int N, double h,
+                           double* x0, double* u_prev, double* traj);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,102 @@
+"""ctypes access to oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Imported only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+always as the checker (never on the product path).  See oracle/mmpc_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+
+NX, NU = 4, 2
+_lib = None
+
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_ip = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.oracle_two_link_jac.argtypes = [_dp, _dp, _dp, _dp, _dp]
+        L.oracle_two_link_xdot.argtypes = [_dp, _dp, _dp]
+        L.oracle_f_lin.argtypes = [C.c_int, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.oracle_nlp_eval.argtypes = [C.c_int, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.oracle_reduced_gradient.argtypes = [C.c_int, C.c_int, C.c_double, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.oracle_solve_batch.argtypes = [
+            C.c_int, C.c_int, C.c_int, C.c_double, C.c_int64, _dp, _dp, _dp, _dp, C.c_int64,
+            C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_double, _dp, _ip, _ip, _dp, _dp, C.c_int,
+        ]
+        L.oracle_solve_batch.restype = C.c_int
+        L.oracle_synth_two_link.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int, C.c_double, _dp, _dp, _dp]
+        _lib = L
+    return _lib
+
+
+def c64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def two_link_jac(x, u):
+    A = np.zeros(16); B = np.zeros(8); xd = np.zeros(4)
+    lib().oracle_two_link_jac(c64(x), c64(u), A, B, xd)
+    return A.reshape(4, 4), B.reshape(4, 2), xd
+
+
+def f_lin(h, A, B, x, u, xdot_init, x_init, u_init):
+    out = np.zeros(4)
+    lib().oracle_f_lin(4, 2, h, c64(A).ravel(), c64(B).ravel(), c64(x), c64(u), c64(xdot_init),
+                       c64(x_init), c64(u_init), out)
+    return out
+
+
+def nlp_eval(N, h, V, u_prev, traj, weights):
+    J = np.zeros(1); g = np.zeros(N * NX)
+    lib().oracle_nlp_eval(0, N, h, c64(V), c64(u_prev), c64(traj).ravel(), c64(weights), J, g)
+    return float(J[0]), g
+
+
+def reduced_gradient(N, h, x0, U, u_prev, traj, weights):
+    g = np.zeros(N * NU)
+    lib().oracle_reduced_gradient(0, N, h, c64(x0), c64(U).ravel(), c64(u_prev), c64(traj).ravel(),
+                                  c64(weights), g)
+    return g
+
+
+def synth(seed, first, B, N, h):
+    x0 = np.zeros((B, NX)); up = np.zeros((B, NU)); tr = np.zeros((B, N, NX))
+    lib().oracle_synth_two_link(seed, first, B, N, h, x0.reshape(-1), up.reshape(-1), tr.reshape(-1))
+    return x0, up, tr
+
+
+def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=50,
+                tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False):
+    x0 = c64(x0).reshape(-1, NX)
+    B = x0.shape[0]
+    NV = NX * (N + 1) + NU * N
+    weights = c64(weights)
+    w_stride = 0 if weights.ndim == 1 else weights.shape[1]
+    V = np.zeros((B, NV)) if V is None else c64(V).reshape(B, NV).copy()
+    st = np.zeros(B, np.int32); it = np.zeros(B, np.int32); kkt = np.zeros(B); J = np.zeros(B)
+    lb = None if u_lb is None else c64(u_lb)
+    ub = None if u_ub is None else c64(u_ub)
+    rc = lib().oracle_solve_batch(
+        0, int(is_linear), N, h, B, x0.reshape(-1), c64(u_prev).reshape(-1), c64(traj).reshape(-1), weights.reshape(-1),
+        w_stride, None if lb is None else lb.ctypes.data, None if ub is None else ub.ctypes.data,
+        max_iter, tol_grad, tol_defect, V.reshape(-1), st, it, kkt, J, nthreads)
+    assert rc == 0
+    return dict(V=V, status=st, iters=it, kkt=kkt, J=J)

@@ -1,0 +1,116 @@
+"""CPU: the C-ABI library loads, exports every function include/mmpc.h declares, and its host-only
+logic (model-file loading per ModelParameters.cpp:52-72, option validation, error reporting) works
+without a GPU.  No compute entry point is called here."""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import pytest
+
+
+def test_library_exports_every_header_symbol(mmpc_mod):
+    L = mmpc_mod.lib()
+    names = mmpc_mod.header_functions()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(L, n), f"libmmpc.so does not export {n}"
+    # and the exported dynamic symbol table says the same (no C++ mangling on the ABI)
+    out = subprocess.run(["nm", "-D", "--defined-only", mmpc_mod.LIB_PATH], capture_output=True, text=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    assert set(names) <= exported
+
+
+def test_library_is_gfx950_code_object(mmpc_mod):
+    """the fat binary carries a gfx950 (MI355X) code object and nothing else"""
+    data = open(mmpc_mod.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in data
+
+
+def test_abi_version_and_defaults(mmpc_mod):
+    assert mmpc_mod.lib().mmpc_abi_version() == 1
+    o = mmpc_mod.default_opts()
+    assert o.max_iter == 50 and o.device == -1
+    assert o.tol_grad == 1e-8 and o.tol_defect == 1e-10
+
+
+def test_load_model_json_like_reference(model_json, mmpc_mod):
+    s = mmpc_mod.Solver(model_json(N=30, h_us=2000))
+    i = s.info
+    assert i.name == b"nonlinear_double_pendulum"
+    assert (i.num_x, i.num_u, i.num_shooting_nodes) == (4, 2, 30)
+    assert i.num_v == 4 * 31 + 2 * 30 == 184 and i.num_g == 120
+    assert i.step_size == pytest.approx(0.002) and i.step_size_us == 2000 and i.timespan_us == 60000
+    assert i.is_linear == 0 and i.model_id == 0
+    # ModelParameters.cpp:66-69: x bounds of exactly +-10e30 become +-inf; u bounds stay +-10e30
+    assert all(i.x_min[k] == float("-inf") and i.x_max[k] == float("inf") for k in range(4))
+    assert all(i.u_min[k] == -10e30 and i.u_max[k] == 10e30 for k in range(2))
+    s.close()
+
+
+def test_load_model_null_bounds_and_linear(tmp_path, mmpc_mod):
+    # nlohmann writes +-inf as null; ex_model_generate.cpp:48-53 style bounds
+    m = {"model": {"name": "linear_double_pendulum", "timespan": 50000, "step_size": 2000, "num_x": 4,
+                   "num_u": 2, "num_shooting_nodes": 25, "x_min": [None] * 4, "u_min": [None] * 2,
+                   "x_max": [None] * 4, "u_max": [None] * 2, "dll_filepath": "x.so", "is_linear": True}}
+    p = tmp_path / "lin.json"
+    p.write_text(json.dumps(m))
+    s = mmpc_mod.Solver(str(p))
+    assert s.info.is_linear == 1 and s.N == 25
+    assert s.info.x_min[0] == float("-inf") and s.info.u_max[1] == 10e30
+
+
+@pytest.mark.parametrize("text,code", [
+    ("{", -3),
+    ('{"model": {"name": "x"}}', -3),
+    ('{"model": {"name": "x", "num_x": 8, "num_u": 4, "num_shooting_nodes": 50, "step_size": 2000}}', -4),
+    ('{"model": {"name": "x", "num_x": 4, "num_u": 2, "num_shooting_nodes": 10, "step_size": 2000,'
+     ' "mmpc_model": "nope"}}', -4),
+    ('{"model": {"name": "x", "num_x": 4, "num_u": 2, "num_shooting_nodes": 10, "step_size": 2000,'
+     ' "u_min": [1, 2, 3]}}', -3),
+])
+def test_bad_model_files_are_api_errors(text, code, mmpc_mod):
+    with pytest.raises(mmpc_mod.MmpcError) as ei:
+        mmpc_mod.Solver(json_text=text)
+    assert ei.value.code == code
+    assert mmpc_mod.lib().mmpc_last_error().decode() != ""
+
+
+def test_missing_file_is_io_error(mmpc_mod, tmp_path):
+    with pytest.raises(mmpc_mod.MmpcError) as ei:
+        mmpc_mod.Solver(str(tmp_path / "nope.json"))
+    assert ei.value.code == -2
+
+
+def test_invalid_opts_rejected(model_json, mmpc_mod):
+    with pytest.raises(mmpc_mod.MmpcError):
+        mmpc_mod.Solver(model_json(), tol_grad=0.0)
+    with pytest.raises(mmpc_mod.MmpcError):
+        mmpc_mod.Solver(model_json(), max_iter=-1)
+
+
+def test_null_and_negative_args(model_json, mmpc_mod):
+    L = mmpc_mod.lib()
+    s = mmpc_mod.Solver(model_json())
+    # B < 0 and null pointers are rejected before any device work
+    assert L.mmpc_solve_batch(s._h, -1, None, None, None, None, 0, None, None, None, None, None, None, None) == -1
+    assert L.mmpc_solve_batch(s._h, 4, None, None, None, None, 0, None, None, None, None, None, None, None) == -1
+    # B == 0 is a no-op success (empty batch)
+    assert L.mmpc_solve_batch(s._h, 0, None, None, None, None, 0, None, None, None, None, None, None, None) == 0
+    assert L.mmpc_destroy(None) == 0
+
+
+def test_status_strings(mmpc_mod):
+    L = mmpc_mod.lib()
+    for k, v in mmpc_mod.STATUS.items():
+        assert L.mmpc_status_string(k).decode() == v
+    assert L.mmpc_status_string(99).decode() == "unknown"
+
+
+def test_flop_model(mmpc_mod):
+    # SURVEY.md 8(d) quotes 288,080 flop/iter for cfg#2 and 96,053 for cfg#1
+    assert abs(mmpc_mod.survey_flops_per_iteration(30) - 288080) <= 1
+    f = mmpc_mod.flops_per_iteration(30)
+    assert f["total"] > 0 and f["gauss_jordan"] > f["hessian"] / 4
