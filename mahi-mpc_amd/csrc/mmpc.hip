@@ -299,7 +299,7 @@ inline unsigned grid1d(int64_t B, int threads) { return static_cast<unsigned>((B
 
 int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
                  const double* weights, int64_t w_stride, const double* u_lb, const double* u_ub, double* V,
-                 int32_t* status, int32_t* iters, double* kkt, hipStream_t stream) {
+                 int32_t* status, int32_t* iters, double* kkt, hipStream_t stream, double* trace = nullptr) {
     const mmpc_model_info& mi = h->info;
     if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
     if (B == 0) return MMPC_OK;
@@ -326,6 +326,7 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.status = status;
     p.iters = iters;
     p.kkt = kkt;
+    p.trace = trace;
     if (mi.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "model not built in");
     // host-side shape checks: the kernel holds one condensed-Hessian row per lane
     const int N = mi.num_shooting_nodes;
@@ -586,5 +587,19 @@ const char* mmpc_status_string(int32_t s) {
 }
 
 const char* mmpc_last_error(void) { return g_last_error.c_str(); }
+
+// Internal diagnostic (not part of include/mmpc.h): as mmpc_solve_batch, plus a per-iteration trace
+// [B][max_iter+1][8] = (||2g||, ||c||, alpha, dphi, phi0, mu, ||du||, accepted).  Device pointers.
+int mmpc_debug_solve_trace(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
+                           const double* weights, int64_t weights_stride, double* V_inout, int32_t* status,
+                           int32_t* iters, double* kkt_res, double* trace, void* stream) {
+    if (!h || B < 0 || !trace) return fail(MMPC_ERR_INVALID_ARG, "bad argument");
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    return launch_solve(h, B, x0, u_prev, traj, weights, weights_stride, nullptr, nullptr, V_inout, status, iters,
+                        kkt_res, reinterpret_cast<hipStream_t>(stream), trace);
+}
 
 }  // extern "C"

@@ -50,6 +50,7 @@ struct SolveParams {
     int32_t* status;
     int32_t* iters;
     double* kkt;
+    double* trace;  // debug: [B][max_iter+1][8] per-iteration diagnostics, or nullptr
 };
 
 enum {
@@ -293,6 +294,11 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
         }
         const double gmax = wave_max(fabs(2.0 * g));
         kkt = fmax(gmax, cmax);
+        double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
+        if (trc && lane == 0) {
+            trc[0] = gmax;
+            trc[1] = cmax;
+        }
         if (__any(nonfinite) || !isfinite(kkt)) {
             status = ST_NONFINITE;
             break;
@@ -541,11 +547,27 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
             Jt = wave_sum(Jt);
             ct = wave_sum(ct);
             const double phit = fma(mu, ct, Jt);
-            if (dphi >= -1e-14 * (1.0 + fabs(phi0)) || phit <= phi0 + 1e-4 * alpha * dphi) {
+            // Noise-aware Armijo: a decrease below ~1e-11 |phi| cannot be resolved by the fp64 merit
+            // (it is a sum of ~200 terms), so such a step is taken whole, and the test allows 1e-13 |phi|
+            // of roundoff.  Without this the test compares noise and alpha collapses.
+            const double noise = 1.0 + fabs(phi0);
+            if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) {
                 accepted = true;
                 break;
             }
             alpha *= 0.5;
+        }
+        if (trc && lane == 0) {
+            trc[2] = alpha;
+            trc[3] = dphi;
+            trc[4] = phi0;
+            trc[5] = mu;
+            trc[6] = wave_max(0.0);
+            trc[7] = accepted ? 1.0 : 0.0;
+        }
+        if (trc) {
+            const double dumax = wave_max(fabs(du));
+            if (lane == 0) trc[6] = dumax;
         }
         if (!accepted) {
             status = ST_LS_FAILED;

@@ -428,7 +428,10 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
             double Jt, ct;
             merit_eval(N, h, s->Xt, s->Ut, u_prev, traj, w, s->Ft, &Jt, &ct);
             double phit = Jt + mu * ct;
-            if (dphi >= -1e-14 * (1.0 + fabs(phi0)) || phit <= phi0 + 1e-4 * alpha * dphi) { accepted = 1; break; }
+            /* noise-aware Armijo (same rule as the HIP kernel): an unresolvable decrease is taken whole,
+             * and the test allows 1e-13 |phi| of roundoff in the merit sum */
+            double noise = 1.0 + fabs(phi0);
+            if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) { accepted = 1; break; }
             alpha *= 0.5;
         }
         if (!accepted) { status = ORACLE_LINESEARCH_FAILED; break; }

@@ -98,7 +98,8 @@ def test_synth_matches_oracle(model_json, mmpc_mod, oracle, torch_cuda):
     ox, ou, ot = oracle.synth(20250213, 12345, B, 30, H)
     np.testing.assert_array_equal(x0.cpu().numpy(), ox)
     np.testing.assert_array_equal(up.cpu().numpy(), ou)
-    np.testing.assert_allclose(tr.cpu().numpy(), ot, rtol=0, atol=4e-15)
+    # sin/cos of the trajectory differ between OCML and glibc by a few ulp (transcendental, not bitwise)
+    np.testing.assert_allclose(tr.cpu().numpy(), ot, rtol=2e-14, atol=2e-15)
 
 
 @pytest.mark.parametrize("which", ["cfg1", "cfg2"])
@@ -134,7 +135,15 @@ def test_cfg2_full_batch_vs_oracle(model_json, mmpc_mod, oracle, torch_cuda):
     gpu = dict(V=V.cpu().numpy(), status=st.cpu().numpy(), iters=it.cpu().numpy(), kkt=kkt.cpu().numpy())
     xo, uo, to = x0.cpu().numpy(), up.cpu().numpy(), tr.cpu().numpy()
     orc = oracle.solve_batch(N, H, xo, uo, to, np.array(WEIGHTS_CFG))
-    assert (gpu["status"] == 0).all()
+    nc = np.where((gpu["status"] != 0) | (orc["status"] != 0))[0]
+    if len(nc):
+        import os
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.savez("gpurun_out/cfg2_nonconverged.npz", idx=nc, x0=xo[nc], u_prev=uo[nc], traj=to[nc],
+                 gpu_status=gpu["status"][nc], gpu_iters=gpu["iters"][nc], gpu_kkt=gpu["kkt"][nc],
+                 orc_status=orc["status"][nc], orc_iters=orc["iters"][nc], orc_kkt=orc["kkt"][nc])
+    assert (gpu["status"] == 0).all(), [(int(i), int(gpu["status"][i]), int(gpu["iters"][i]), float(gpu["kkt"][i]),
+                                         int(orc["status"][i]), int(orc["iters"][i]), float(orc["kkt"][i])) for i in nc]
     assert (gpu["kkt"] <= 1e-8).all()
     dump_inputs.update(x0=xo, u_prev=uo, traj=to)
     import os
