@@ -588,6 +588,18 @@ const char* mmpc_status_string(int32_t s) {
 
 const char* mmpc_last_error(void) { return g_last_error.c_str(); }
 
+// Internal diagnostic: per-phase s_memtime cycle totals of the SQP kernel (all zero unless the library
+// was built with -DMMPC_PHASE_TIMING, i.e. lib/libmmpc_timing.so).  out[15] = number of waves.
+int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) {
+    if (!out16) return fail(MMPC_ERR_INVALID_ARG, "null");
+    MMPC_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mmpc_phase_cycles), 16 * sizeof(unsigned long long)));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        MMPC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z)));
+    }
+    return MMPC_OK;
+}
+
 // Internal diagnostic (not part of include/mmpc.h): as mmpc_solve_batch, plus a per-iteration trace
 // [B][max_iter+1][8] = (||2g||, ||c||, alpha, dphi, phi0, mu, ||du||, accepted).  Device pointers.
 int mmpc_debug_solve_trace(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,

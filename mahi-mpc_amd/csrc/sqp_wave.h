@@ -26,7 +26,7 @@
 #include "models.h"
 
 #ifndef MMPC_WAVES_PER_SIMD
-#define MMPC_WAVES_PER_SIMD 3
+#define MMPC_WAVES_PER_SIMD 2
 #endif
 
 namespace mmpc {
@@ -74,13 +74,27 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
     return __hiloint2double(hi, lo);
 }
 
+// DPP move of a double (both halves), all lanes active
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
 // broadcast lane Q of each quad to the whole quad (DPP quad_perm [Q,Q,Q,Q])
 template <int Q>
 __device__ __forceinline__ double quad_bcast(double v) {
-    constexpr int ctrl = Q | (Q << 2) | (Q << 4) | (Q << 6);
-    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), ctrl, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), ctrl, 0xF, 0xF, false);
-    return __hiloint2double(hi, lo);
+    return dpp_d<Q | (Q << 2) | (Q << 4) | (Q << 6)>(v);
+}
+// rotate within each 16-lane row by 4*S lanes (DPP row_ror:4S); the source lane is queried at run time
+// with the same instruction, so nothing depends on the rotation direction
+template <int S>
+__device__ __forceinline__ double row_rot4(double v) {
+    return dpp_d<0x120 + 4 * S>(v);
+}
+template <int S>
+__device__ __forceinline__ int row_rot4_src(int lane) {
+    return __builtin_amdgcn_mov_dpp(lane, 0x120 + 4 * S, 0xF, 0xF, false);
 }
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -103,6 +117,31 @@ __device__ __forceinline__ double rcp_nr(double a) {
     return fma(r, e, r);
 }
 
+// ---------------- diagnostic phase timing (separate build, -DMMPC_PHASE_TIMING) ----------------
+// s_memtime stamps between phases, accumulated per wave and added to a device table at exit.
+// Only the diagnostic library libmmpc_timing.so is built with it; its run time is not quoted.
+__device__ unsigned long long g_mmpc_phase_cycles[16];
+#ifdef MMPC_PHASE_TIMING
+#define MMPC_PHASE_DECL unsigned long long ph_acc[10] = {0}, ph_t = __builtin_amdgcn_s_memtime();
+#define MMPC_PHASE(i)                                        \
+    do {                                                     \
+        __builtin_amdgcn_sched_barrier(0);                   \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+        ph_acc[i] += t_ - ph_t;                              \
+        ph_t = t_;                                           \
+        __builtin_amdgcn_sched_barrier(0);                   \
+    } while (0)
+#define MMPC_PHASE_FLUSH                                                          \
+    if (lane0 == 0) {                                                             \
+        for (int q_ = 0; q_ < 10; ++q_) atomicAdd(&g_mmpc_phase_cycles[q_], ph_acc[q_]); \
+        atomicAdd(&g_mmpc_phase_cycles[15], 1ull);                                \
+    }
+#else
+#define MMPC_PHASE_DECL
+#define MMPC_PHASE(i)
+#define MMPC_PHASE_FLUSH
+#endif
+
 // ---------------- the kernel ----------------
 template <class Model, int NMAX>
 __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(SolveParams p) {
@@ -111,26 +150,27 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
     static_assert(NX == 4, "quad-DPP recursions assume NX == 4");
     static_assert(MMAX <= 64, "one Hessian row per lane");
 
-    __shared__ double sX[(NMAX + 1) * NX];
-    __shared__ double sU[NMAX * NU];
-    __shared__ double sF[NMAX * NX];
-    __shared__ double sA[NMAX * NX * NX];
-    __shared__ double sB[NMAX * NX * NU];
-    __shared__ double sZ[NMAX * NU * NX];
-    __shared__ double sC[NMAX * NX];
-    __shared__ double sE[NMAX * NX];
-    __shared__ double sR[NMAX * NX];
-    __shared__ double sLam[(NMAX + 1) * NX];
-    __shared__ double sDX[(NMAX + 1) * NX];
-    __shared__ double sDU[MMAX];
-    __shared__ double sP[NX * NX];
-    __shared__ double sT[NX * NX];
-    __shared__ double sW[NX + 2 * NU];
-    __shared__ double sLin[NX * NX + NX * NU + NX];
-    __shared__ double sUp[NU];
+    __shared__ __attribute__((aligned(16))) double sX[(NMAX + 1) * NX];
+    __shared__ __attribute__((aligned(16))) double sU[NMAX * NU];
+    __shared__ __attribute__((aligned(16))) double sF[NMAX * NX];
+    __shared__ __attribute__((aligned(16))) double sA[NMAX * NX * NX];
+    __shared__ __attribute__((aligned(16))) double sB[NMAX * NX * NU];
+    __shared__ __attribute__((aligned(16))) double sZ[NMAX * NU * NX];
+    __shared__ __attribute__((aligned(16))) double sC[NMAX * NX];
+    __shared__ __attribute__((aligned(16))) double sE[NMAX * NX];
+    __shared__ __attribute__((aligned(16))) double sR[NMAX * NX];
+    __shared__ __attribute__((aligned(16))) double sLam[(NMAX + 1) * NX];
+    __shared__ __attribute__((aligned(16))) double sDX[(NMAX + 1) * NX];
+    __shared__ __attribute__((aligned(16))) double sDU[MMAX];
+    __shared__ __attribute__((aligned(16))) double sPiv[66];
+    __shared__ __attribute__((aligned(16))) double sDiag[64];
+    __shared__ __attribute__((aligned(16))) double sW[NX + 2 * NU];
+    __shared__ __attribute__((aligned(16))) double sLin[NX * NX + NX * NU + NX];
+    __shared__ __attribute__((aligned(16))) double sUp[NU];
 
     const int lane0 = threadIdx.x;
     const int lane = lane0;
+    MMPC_PHASE_DECL
     const int64_t inst = blockIdx.x;
     const int N = p.N;
     const int M = N * NU;
@@ -187,6 +227,7 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
     int status = ST_MAX_ITER;
     int it = 0;
     double kkt = 0.0, mu = 0.0;
+    MMPC_PHASE(0);
 
     for (it = 0; it <= p.max_iter; ++it) {
         // Re-derive the lane id opaquely each iteration: otherwise LICM hoists every lane-dependent
@@ -245,39 +286,108 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
         }
         __syncthreads();
         cmax = wave_max(cmax);
+        MMPC_PHASE(1);
 
         const double Qa = sW[qa];
         // ---- 2. forward d / e (all quads redundant, quad 0 stores) ----
         {
             double d = 0.0;  // d_0 = x0 - x_0 = 0 (x_0 is pinned)
+            // operands of step k+1 are loaded while step k computes (the recursion is latency-bound)
+            double2 a01 = reinterpret_cast<const double2*>(sA + qa * NX)[0];
+            double2 a23 = reinterpret_cast<const double2*>(sA + qa * NX)[1];
+            double fr = sF[qa] - sR[qa], cc = sC[qa];
             for (int k = 0; k < N; ++k) {
-                const double* Ak = sA + k * NX * NX + qa * NX;
+                const int kn = (k + 1 < N) ? k + 1 : k;
+                const double2 na01 = reinterpret_cast<const double2*>(sA + kn * NX * NX + qa * NX)[0];
+                const double2 na23 = reinterpret_cast<const double2*>(sA + kn * NX * NX + qa * NX)[1];
+                const double nfr = sF[kn * NX + qa] - sR[kn * NX + qa], ncc = sC[kn * NX + qa];
                 const double d0 = quad_bcast<0>(d), d1 = quad_bcast<1>(d), d2 = quad_bcast<2>(d),
                              d3 = quad_bcast<3>(d);
-                const double ad = fma(Ak[0], d0, fma(Ak[1], d1, fma(Ak[2], d2, Ak[3] * d3)));
-                if (lane < NX) sE[k * NX + qa] = sF[k * NX + qa] + ad - sR[k * NX + qa];
-                d = ad + sC[k * NX + qa];
+                const double ad = fma(a01.x, d0, a01.y * d1) + fma(a23.x, d2, a23.y * d3);
+                if (lane < NX) sE[k * NX + qa] = fr + ad;
+                d = ad + cc;
+                a01 = na01;
+                a23 = na23;
+                fr = nfr;
+                cc = ncc;
             }
         }
         __syncthreads();
+        MMPC_PHASE(2);
 
-        // ---- 3. adjoint lam and reduced gradient ----
+        // ---- 3+4. fused backward sweep (no LDS round trips, no barriers inside) ----
+        //   lanes 0..15  (row 0): P_{i+1}[pa][pb] -> Z_i = B_i^T P_{i+1}, P_i = Q + A_i^T P_{i+1} A_i
+        //                         rows of P/T via quad_perm, columns via row_ror:4/8/12
+        //   lanes 16..19 (quad 4): adjoint lam_i = Q e_{i-1} + A_i^T lam_{i+1}
         double lmax;
         {
-            double lam = Qa * sE[(N - 1) * NX + qa];
-            if (lane < NX) sLam[N * NX + qa] = lam;
-            lmax = fabs(lam);
-            for (int k = N - 1; k >= 1; --k) {
-                const double l0 = quad_bcast<0>(lam), l1 = quad_bcast<1>(lam), l2 = quad_bcast<2>(lam),
-                             l3 = quad_bcast<3>(lam);
-                const double* Ak = sA + k * NX * NX + qa;  // column qa of A_k
-                lam = fma(Qa, sE[(k - 1) * NX + qa],
-                          fma(Ak[0], l0, fma(Ak[NX], l1, fma(Ak[2 * NX], l2, Ak[3 * NX] * l3))));
-                if (lane < NX) sLam[k * NX + qa] = lam;
-                lmax = fmax(lmax, fabs(lam));
+            const int pa = (lane >> 2) & 3, pb = lane & 3;
+            // row index of the value each lane receives from row_ror:4s (s = 1,2,3)
+            const int c1 = (row_rot4_src<1>(lane) >> 2) & 3;
+            const int c2 = (row_rot4_src<2>(lane) >> 2) & 3;
+            const int c3 = (row_rot4_src<3>(lane) >> 2) & 3;
+            const bool lam_lane = (lane >> 2) == 4;
+            double P = (pa == pb) ? sW[pa] : 0.0;  // P_N = Q
+            double lam = Qa * sE[(N - 1) * NX + qa];  // lam_N
+            if (lam_lane) sLam[N * NX + qa] = lam;
+            lmax = lam_lane ? fabs(lam) : 0.0;
+            const int zr = pa < NU ? pa : NU - 1;  // Z row handled by this lane (lanes pa < NU store it)
+            // per-lane operands of step i: column pb of A_i (for T), A_i[c][pa] (for P), B_i[c][zr] (for Z),
+            // column qa of A_i (for lam), e_{i-1}[qa]
+            struct Ops {
+                double aT[4], aP[4], bZ[4], aL[4], e;
+            };
+            auto load_ops = [&](int i, Ops& o) {
+                const double* Ai = sA + i * NX * NX;
+                const double* Bi = sB + i * NX * NU;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    o.aT[c] = Ai[c * NX + pb];
+                    o.aL[c] = Ai[c * NX + qa];
+                }
+                o.aP[0] = Ai[pa * NX + pa];
+                o.aP[1] = Ai[c1 * NX + pa];
+                o.aP[2] = Ai[c2 * NX + pa];
+                o.aP[3] = Ai[c3 * NX + pa];
+                o.bZ[0] = Bi[pa * NU + zr];
+                o.bZ[1] = Bi[c1 * NU + zr];
+                o.bZ[2] = Bi[c2 * NU + zr];
+                o.bZ[3] = Bi[c3 * NU + zr];
+                o.e = sE[(i >= 1 ? i - 1 : 0) * NX + qa];
+            };
+            Ops cur;
+            load_ops(N - 1, cur);
+            const double pq = (pa == pb) ? sW[pa] : 0.0;
+            for (int i = N - 1; i >= 0; --i) {
+                Ops nxt;
+                load_ops(i >= 1 ? i - 1 : 0, nxt);
+                // column pb of P_{i+1}: own value is row pa, rotations give rows c1..c3
+                const double P1 = row_rot4<1>(P), P2 = row_rot4<2>(P), P3 = row_rot4<3>(P);
+                if (lane < 16 && pa < NU) {
+                    const double z = fma(cur.bZ[3], P3, fma(cur.bZ[2], P2, fma(cur.bZ[1], P1, cur.bZ[0] * P)));
+                    sZ[i * NU * NX + pa * NX + pb] = z;
+                }
+                // T = P_{i+1} A_i : row pa of P by quad broadcast
+                const double r0 = quad_bcast<0>(P), r1 = quad_bcast<1>(P), r2 = quad_bcast<2>(P), r3 = quad_bcast<3>(P);
+                const double T = fma(r0, cur.aT[0], r1 * cur.aT[1]) + fma(r2, cur.aT[2], r3 * cur.aT[3]);
+                // P_i = Q + A_i^T T : column pb of T by row rotations
+                const double T1 = row_rot4<1>(T), T2 = row_rot4<2>(T), T3 = row_rot4<3>(T);
+                P = pq + (fma(cur.aP[0], T, cur.aP[1] * T1) + fma(cur.aP[2], T2, cur.aP[3] * T3));
+                // adjoint (quad 4)
+                if (i >= 1) {
+                    const double l0 = quad_bcast<0>(lam), l1 = quad_bcast<1>(lam), l2 = quad_bcast<2>(lam),
+                                 l3 = quad_bcast<3>(lam);
+                    lam = fma(Qa, cur.e, fma(cur.aL[0], l0, cur.aL[1] * l1) + fma(cur.aL[2], l2, cur.aL[3] * l3));
+                    if (lam_lane) {
+                        sLam[i * NX + qa] = lam;
+                        lmax = fmax(lmax, fabs(lam));
+                    }
+                }
+                cur = nxt;
             }
         }
         __syncthreads();
+        MMPC_PHASE(4);
         const int si = lane / NU, sr = lane - (lane / NU) * NU;  // Hessian row lane = (stage si, input sr)
         const bool row_valid = lane < M;
         double g = 0.0;
@@ -311,43 +421,15 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
             status = ST_MAX_ITER;
             break;
         }
-
-        // ---- 4. Lyapunov recursion P, Z_i = B_i^T P_{i+1} (lanes 0..15) ----
-        {
-            const int pa = (lane >> 2) & 3, pb = lane & 3;
-            double P = (pa == pb) ? sW[pa] : 0.0;  // P_N = Q
-            for (int i = N - 1; i >= 0; --i) {
-                if (lane < 16) sP[lane] = P;
-                __syncthreads();
-                if (lane < 16) {
-                    const double* Ai = sA + i * NX * NX;
-                    const double* Bi = sB + i * NX * NU;
-                    if (pa < NU) {
-                        double z = 0.0;
-#pragma unroll
-                        for (int c = 0; c < NX; ++c) z = fma(Bi[c * NU + pa], sP[c * NX + pb], z);
-                        sZ[i * NU * NX + pa * NX + pb] = z;
-                    }
-                    double t = 0.0;
-#pragma unroll
-                    for (int c = 0; c < NX; ++c) t = fma(sP[pa * NX + c], Ai[c * NX + pb], t);
-                    sT[lane] = t;
-                }
-                __syncthreads();
-                if (lane < 16) {
-                    const double* Ai = sA + i * NX * NX;
-                    double pn = (pa == pb) ? sW[pa] : 0.0;
-#pragma unroll
-                    for (int c = 0; c < NX; ++c) pn = fma(Ai[c * NX + pa], sT[c * NX + pb], pn);
-                    P = pn;
-                }
-            }
-        }
-        __syncthreads();
+        MMPC_PHASE(3);
 
         // ---- 5. condensed Hessian, one row per lane ----
+        // lower part (j <= si): t_j = t_{j+1} A_{j+1} + d_j z,  H_ij = t_j B_j   (t_j == 0 for j > si)
+        // upper part (j >  si): w_j = A_j v_{j-1},  H_ij = Z_j w_j,  v_j = w_j + d_j b  (w_j == 0 for j <= si)
+        // with d_j = [j == si]; the two parts never overlap, so they simply add (no selects).  The D^T R D + Rm
+        // band (ModelGenerator.cpp:216-221) rides on the same indicators: diagonal at d_j, sub/super
+        // diagonals at d_{j+1} (lower sweep) and d_{j-1} (upper sweep).
         double hrow[MMAX];
-#ifndef MMPC_DBG_NO_HBUILD
         {
             double z[NX], bcol[NX];
 #pragma unroll
@@ -355,122 +437,190 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
                 z[q] = row_valid ? sZ[si * NU * NX + sr * NX + q] : 0.0;
                 bcol[q] = row_valid ? sB[si * NX * NU + q * NU + sr] : 0.0;
             }
-            // lower part, j <= si: t_(j) = Z_i Phi_{i+1,j+1}; t_(si) = z; t_(j) = t_(j+1) A_{j+1}
+            const int srr = sr < NU ? sr : 0;
+            const double Rr = sW[NX + srr], Rmr = sW[NX + NU + srr];
+            const double dterm = Rr * ((si + 1 < N) ? 2.0 : 1.0) + Rmr;
+            double wdiag[NU], woff[NU];
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                wdiag[c] = (c == sr) ? dterm : 0.0;
+                woff[c] = (c == sr) ? -Rr : 0.0;
+            }
             double t[NX] = {0.0, 0.0, 0.0, 0.0};
+            double dprev = 0.0;  // d_{j+1}
 #pragma unroll
             for (int j = NMAX - 1; j >= 0; --j) {
+                int jj = j;
+                asm volatile("" : "+s"(jj));
+                const double dj = (si == jj) ? 1.0 : 0.0;
                 if (j < NMAX - 1) {
                     const double* A1 = sA + (j + 1) * NX * NX;
                     double tn[NX];
 #pragma unroll
                     for (int q = 0; q < NX; ++q)
-                        tn[q] = fma(t[0], A1[0 * NX + q],
-                                    fma(t[1], A1[1 * NX + q], fma(t[2], A1[2 * NX + q], t[3] * A1[3 * NX + q])));
+                        tn[q] = fma(t[3], A1[3 * NX + q],
+                                    fma(t[2], A1[2 * NX + q], fma(t[1], A1[1 * NX + q], fma(t[0], A1[0 * NX + q], dj * z[q]))));
 #pragma unroll
                     for (int q = 0; q < NX; ++q) t[q] = tn[q];
-                }
-                const bool at = (si == j);
+                } else {
 #pragma unroll
-                for (int q = 0; q < NX; ++q) t[q] = at ? z[q] : t[q];
+                    for (int q = 0; q < NX; ++q) t[q] = dj * z[q];
+                }
                 const double* Bj = sB + j * NX * NU;
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
-                    hrow[j * NU + c] = fma(t[0], Bj[0 * NU + c],
-                                           fma(t[1], Bj[1 * NU + c], fma(t[2], Bj[2 * NU + c], t[3] * Bj[3 * NU + c])));
+                    const double base = fma(dprev, woff[c], dj * wdiag[c]);
+                    hrow[j * NU + c] = fma(t[3], Bj[3 * NU + c],
+                                           fma(t[2], Bj[2 * NU + c], fma(t[1], Bj[1 * NU + c], fma(t[0], Bj[0 * NU + c], base))));
                     MMPC_PIN(hrow[j * NU + c]);
                 }
 #pragma unroll
                 for (int q = 0; q < NX; ++q) MMPC_PIN(t[q]);
+                dprev = dj;
             }
-            // upper part, j > si: v_(j) = Phi_{j+1,i+1} B_i[:,r]; v_(si) = bcol; v_(j) = A_j v_(j-1)
             double v[NX] = {0.0, 0.0, 0.0, 0.0};
+            dprev = 0.0;  // d_{j-1}
 #pragma unroll
             for (int j = 0; j < NMAX; ++j) {
+                int jj = j;
+                asm volatile("" : "+s"(jj));
+                const double dj = (si == jj) ? 1.0 : 0.0;
                 const double* Aj = sA + j * NX * NX;
-                double vn[NX];
+                double w[NX];
 #pragma unroll
                 for (int q = 0; q < NX; ++q)
-                    vn[q] = fma(Aj[q * NX + 0], v[0],
-                                fma(Aj[q * NX + 1], v[1], fma(Aj[q * NX + 2], v[2], Aj[q * NX + 3] * v[3])));
-                const bool at = (si == j);
-#pragma unroll
-                for (int q = 0; q < NX; ++q) v[q] = at ? bcol[q] : vn[q];
+                    w[q] = fma(Aj[q * NX + 3], v[3], fma(Aj[q * NX + 2], v[2], fma(Aj[q * NX + 1], v[1], Aj[q * NX + 0] * v[0])));
                 const double* Zj = sZ + j * NU * NX;
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
-                    const double hv = fma(Zj[c * NX + 0], v[0],
-                                          fma(Zj[c * NX + 1], v[1], fma(Zj[c * NX + 2], v[2], Zj[c * NX + 3] * v[3])));
-                    hrow[j * NU + c] = (j > si) ? hv : hrow[j * NU + c];
+                    hrow[j * NU + c] = fma(Zj[c * NX + 3], w[3],
+                                           fma(Zj[c * NX + 2], w[2], fma(Zj[c * NX + 1], w[1],
+                                               fma(Zj[c * NX + 0], w[0], fma(dprev, woff[c], hrow[j * NU + c])))));
                     MMPC_PIN(hrow[j * NU + c]);
                 }
 #pragma unroll
-                for (int q = 0; q < NX; ++q) MMPC_PIN(v[q]);
-            }
-            // D^T R D + Rm (ModelGenerator.cpp:216-221), padding rows/cols -> identity
-            const double Rr = sW[NX + (sr < NU ? sr : 0)], Rmr = sW[NX + NU + (sr < NU ? sr : 0)];
-            const double dterm = Rr * ((si + 1 < N) ? 2.0 : 1.0) + Rmr;
-#pragma unroll
-            for (int cidx = 0; cidx < MMAX; ++cidx) {
-                double hv = hrow[cidx];
-                hv += (cidx == lane) ? dterm : 0.0;
-                hv -= (cidx == lane - NU || cidx == lane + NU) ? Rr : 0.0;
-                if (cidx >= M) hv = 0.0;
-                if (!row_valid) hv = (cidx == lane) ? 1.0 : 0.0;
-                hrow[cidx] = hv;
+                for (int q = 0; q < NX; ++q) {
+                    v[q] = fma(dj, bcol[q], w[q]);
+                    MMPC_PIN(v[q]);
+                }
+                dprev = dj;
             }
         }
-#else
-        for (int cidx = 0; cidx < MMAX; ++cidx) hrow[cidx] = (cidx == lane) ? 2.0 : sDU[cidx];
-#endif
-
+        MMPC_PHASE(5);
         // ---- 6. Gauss-Jordan on [H | -g] ----
+        // The trailing block stays symmetric under elimination, so the pivot ROW entries a_kj (j > k)
+        // equal the pivot COLUMN entries a_jk that lane j holds in register k: one ds_write_b64 per step
+        // publishes the pivot row, and every update is an FMA with a broadcast LDS operand.  The row is
+        // written at an offset that makes every pair (k+1+2q, k+2+2q) 16-byte aligned (ds_read_b128), and
+        // the reads run two 8-value chunks ahead of the FMAs (LDS latency hidden inside the wave).
         double rhs = row_valid ? -g : 0.0;
-        double diag = 1.0;
         bool fact_bad = false;
-#ifndef MMPC_DBG_NO_GJ
-        for (int k = 0; k < M; ++k) {
-            const double akk = readlane_d(hrow[0], k);
-            fact_bad |= !(akk > 0.0) || !isfinite(akk);
-            const double inv = rcp_nr(akk);
-            const double mlt = (lane == k) ? 0.0 : hrow[0] * inv;
-            diag = (lane == k) ? akk : diag;
-            rhs = fma(-mlt, readlane_d(rhs, k), rhs);
-            const int W1 = M - k - 1;  // columns left of the window after this step
 #pragma unroll
-            for (int j = 0; j < MMAX - 1; ++j) {
-                if ((j & 7) == 0 && j >= W1) break;
-                hrow[j] = fma(-mlt, readlane_d(hrow[j + 1], k), hrow[j + 1]);
-                MMPC_PIN(hrow[j]);
+        for (int k = 0; k < MMAX; ++k) {
+            if (k < M) {
+                constexpr int CH = 8;
+                double* piv = sPiv + (((k & 1) ^ 1));  // (k+1+off) even -> aligned pairs
+                const double col = hrow[k];
+                piv[lane] = col;
+                __builtin_amdgcn_wave_barrier();
+                int ko = k;  // opaque copy: keeps the lane == k compare inside this step (no SGPR-mask hoisting)
+                asm volatile("" : "+s"(ko));
+                const double akk = reinterpret_cast<const double2*>(sPiv)[(((k & 1) ^ 1) + k - 1) >> 1].y;
+                const int NCH = (MMAX - 1 - k + CH - 1) / CH;
+                const double2* piv2 = reinterpret_cast<const double2*>(sPiv);  // 16-B aligned pairs
+                const int off = (k & 1) ^ 1;
+                double preA[CH], preB[CH];
+#pragma unroll
+                for (int q = 0; q < CH; q += 2) {
+                    const int j0 = k + 1 + q, j1 = k + 1 + CH + q;
+                    if (j0 < MMAX) {
+                        const double2 v = piv2[(off + j0) >> 1];
+                        preA[q] = v.x;
+                        preA[q + 1] = v.y;
+                    }
+                    if (j1 < MMAX) {
+                        const double2 v = piv2[(off + j1) >> 1];
+                        preB[q] = v.x;
+                        preB[q + 1] = v.y;
+                    }
+                }
+                fact_bad |= !(akk > 0.0) || !isfinite(akk);
+                const double inv = rcp_nr(akk);
+                const double mlt = (lane == ko) ? 0.0 : col * inv;
+                if (lane == 0) sDiag[k] = akk;
+                rhs = fma(-mlt, readlane_d(rhs, k), rhs);
+#pragma unroll
+                for (int c = 0; c < NCH; ++c) {
+                    double cur[CH];
+#pragma unroll
+                    for (int q = 0; q < CH; ++q) cur[q] = (c & 1) ? preB[q] : preA[q];
+#pragma unroll
+                    for (int q = 0; q < CH; q += 2) {
+                        const int jn = k + 1 + (c + 2) * CH + q;  // refill the buffer just consumed
+                        if (c + 2 < NCH && jn < MMAX) {
+                            const double2 v = piv2[(off + jn) >> 1];
+                            if (c & 1) {
+                                preB[q] = v.x;
+                                preB[q + 1] = v.y;
+                            } else {
+                                preA[q] = v.x;
+                                preA[q + 1] = v.y;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int q = 0; q < CH; ++q) {
+                        const int j = k + 1 + c * CH + q;
+                        if (j < MMAX) hrow[j] = fma(-mlt, cur[q], hrow[j]);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
             }
         }
-#else
-        for (int j = 0; j < MMAX; ++j) rhs += hrow[j] * sDU[j];
-#endif
         if (fact_bad) {
             status = ST_FACT_FAILED;
             break;
         }
-        const double du = row_valid ? rhs / diag : 0.0;
+        __syncthreads();
+        const double du = row_valid ? rhs / sDiag[lane] : 0.0;
         if (row_valid) sDU[lane] = du;
         __syncthreads();
+        MMPC_PHASE(6);
 
         // ---- 7. dx forward ----
         {
             double dx = 0.0;
             if (lane < NX) sDX[qa] = 0.0;
+            auto ld = [&](int k, double2& a01, double2& a23, double2& b01, double& cc, double2& du01) {
+                a01 = reinterpret_cast<const double2*>(sA + k * NX * NX + qa * NX)[0];
+                a23 = reinterpret_cast<const double2*>(sA + k * NX * NX + qa * NX)[1];
+                b01 = reinterpret_cast<const double2*>(sB + k * NX * NU + qa * NU)[0];
+                cc = sC[k * NX + qa];
+                du01 = reinterpret_cast<const double2*>(sDU + k * NU)[0];
+            };
+            static_assert(NU == 2, "dx recursion packs the two controls of a stage");
+            double2 a01, a23, b01, du01;
+            double cc;
+            ld(0, a01, a23, b01, cc, du01);
             for (int k = 0; k < N; ++k) {
-                const double* Ak = sA + k * NX * NX + qa * NX;
-                const double* Bk = sB + k * NX * NU + qa * NU;
+                double2 na01, na23, nb01, ndu01;
+                double ncc;
+                ld((k + 1 < N) ? k + 1 : k, na01, na23, nb01, ncc, ndu01);
                 const double x0v = quad_bcast<0>(dx), x1v = quad_bcast<1>(dx), x2v = quad_bcast<2>(dx),
                              x3v = quad_bcast<3>(dx);
-                double dn = fma(Ak[0], x0v, fma(Ak[1], x1v, fma(Ak[2], x2v, fma(Ak[3], x3v, sC[k * NX + qa]))));
-#pragma unroll
-                for (int c = 0; c < NU; ++c) dn = fma(Bk[c], sDU[k * NU + c], dn);
+                const double bu = fma(b01.x, du01.x, fma(b01.y, du01.y, cc));
+                const double dn = (fma(a01.x, x0v, a01.y * x1v) + fma(a23.x, x2v, a23.y * x3v)) + bu;
                 if (lane < NX) sDX[(k + 1) * NX + qa] = dn;
                 dx = dn;
+                a01 = na01;
+                a23 = na23;
+                b01 = nb01;
+                cc = ncc;
+                du01 = ndu01;
             }
         }
         __syncthreads();
+        MMPC_PHASE(7);
 
         // ---- 8. l1-merit Armijo line search ----
         mu = fmax(mu, 4.0 * wave_max(lmax) + 1.0);
@@ -576,7 +726,9 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
         for (int i = NX + lane; i < (N + 1) * NX; i += 64) sX[i] = fma(alpha, sDX[i], sX[i]);
         if (lane < M) sU[lane] = fma(alpha, sDU[lane], sU[lane]);
         __syncthreads();
+        MMPC_PHASE(8);
     }
+    MMPC_PHASE(3);
 
     // ---- bounds check (box constraints are reported, not yet enforced) ----
     if (status == ST_CONVERGED && (p.u_lb || p.u_ub)) {
@@ -611,6 +763,8 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
         if (p.iters) p.iters[inst] = it;
         if (p.kkt) p.kkt[inst] = kkt;
     }
+    MMPC_PHASE(9);
+    MMPC_PHASE_FLUSH
 }
 
 }  // namespace mmpc

@@ -22,7 +22,7 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)                      # mahi-mpc_amd/
 REPO = os.path.dirname(ROOT)
-LIB_PATH = os.path.join(ROOT, "lib", "libmmpc.so")
+LIB_PATH = os.environ.get("MMPC_LIB_PATH") or os.path.join(ROOT, "lib", "libmmpc.so")
 HEADER_PATH = os.path.join(REPO, "include", "mmpc.h")
 
 OK = 0
