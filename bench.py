@@ -77,6 +77,7 @@ def main():
     import torch
     import torch.distributed as dist
     import mmpc
+    import mmpc.dist as mdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -103,7 +104,8 @@ def main():
     it = torch.empty(B, dtype=torch.int32, device=dev)
     kkt = torch.empty(B, **f64)
     stream = torch.cuda.current_stream(dev)
-    solver.synth(SEED, rank * B, B, x0, up, tr, stream=stream.cuda_stream)
+    first, _ = mdist.shard(B, rank)
+    solver.synth(SEED, first, B, x0, up, tr, stream=stream.cuda_stream)
 
     def step():
         V.zero_()   # cold start (reference first call: v_init = 0, ModelControl.cpp:29-50)
@@ -127,24 +129,19 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = mdist.max_over_ranks(elapsed, device=dev)
 
     iters = it.cpu().numpy()
     status = st.cpu().numpy()
-    conv = int((status == 0).sum())
-    if world > 1:
-        c = torch.tensor([conv], dtype=torch.int64, device=dev)
-        dist.all_reduce(c)
-        conv = int(c.item())
+    conv = int(mdist.sum_over_ranks(int((status == 0).sum()), device=dev))
     total = B * world * args.steps
     value = total / elapsed
-    fl = mmpc.flops_per_iteration(N)
-    flops_launch = float(iters.sum()) * fl["total"]            # this rank's kernel, algorithmic
-    achieved = flops_launch / (kern_ms * 1e-3) / 1e12
+    # algorithmic flops of one launch = SURVEY.md 8(d) per-iteration figure x the SQP iterations the
+    # launch's instances actually took (unit of work = 1 solve = sum over its iterations)
     survey_fl = float(iters.sum()) * mmpc.survey_flops_per_iteration(N)
+    achieved = survey_fl / (kern_ms * 1e-3) / 1e12
+    fl = mmpc.flops_per_iteration(N)
+    own_fl = float(iters.sum()) * fl["total"]
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -176,8 +173,9 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "sqp_wave_kernel<TwoLinkArm,30>",
-                     "flops_per_iter": fl["total"],
-                     "survey_8d_equivalent_tflops": survey_fl / (kern_ms * 1e-3) / 1e12},
+                     "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N),
+                     "flops_per_iter_kernel_own_count": fl["total"],
+                     "kernel_own_count_tflops": own_fl / (kern_ms * 1e-3) / 1e12},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(N, h, args.cpu_seconds)

@@ -1,0 +1,60 @@
+// Closed-loop cfg#1 through the drop-in C++ API: the reference's examples/model_control_example.cpp:8-154
+// with the thread example's weights (thread_model_control_example.cpp:24-25) and an explicit Rm.
+// ModelGenerator writes the model file (ex_model_generate.cpp:59-71 with N from the command line), then
+// calc_u runs every 5th tick (model_control_example.cpp:74-76) and the Euler plant uses the device
+// linearisation's x_dot (model_control_example.cpp:81-86).  Prints one CSV line per tick:
+//   t, q0..q3, T0, T1, status, iterations
+#include <Mahi/Mpc.hpp>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../../../include/mmpc.h"
+
+using namespace mahi::mpc;
+
+int main(int argc, char** argv) {
+    const int N = argc > 1 ? std::atoi(argv[1]) : 20;
+    const double sim_seconds = argc > 2 ? std::atof(argv[2]) : 0.2;
+    const bool linear = argc > 3 && argv[3][0] == 'l';
+    const std::string name = linear ? "linear_double_pendulum" : "nonlinear_double_pendulum";
+    ModelParameters mp(name, 4, 2, mahi::util::milliseconds(2), N, linear);
+    ModelGenerator gen(mp, "two_link_arm");
+    gen.create_model();
+    gen.generate_c_code();
+    gen.compile_model();
+
+    ModelControl mc(name, {10, 1, 5, 5}, {5, 5}, {0.01, 0.01});
+    const int nx = mc.model_parameters.num_x;
+    const double h = mc.model_parameters.step_size.as_seconds();
+    std::vector<double> state(4, 0.0), control(2, 0.0);
+    mmpc_handle* lin = nullptr;  // plant model: <name>_get_x_dot_init replacement
+    if (mmpc_create((name + ".json").c_str(), nullptr, &lin) != MMPC_OK) return 2;
+    const double PI = 3.14159265358979323846, sin_amp = 1.0, sin_freq = 1.0;
+    double t = 0.0;
+    int cycle = 0;
+    while (t < sim_seconds - 1e-12) {
+        std::vector<double> traj;
+        double tt = t;
+        for (int i = 0; i < N; i++) {  // model_control_example.cpp:58-68
+            for (int j = 0; j < nx; j++) {
+                if (j < nx / 2) traj.push_back(((j % 2 == 0) ? 1.0 : -1.0) * sin_amp * std::sin(2 * PI * sin_freq * tt));
+                else traj.push_back((((j - nx / 2) % 2 == 0) ? 1.0 : -1.0) * sin_amp * 2 * PI * sin_freq * std::cos(2 * PI * sin_freq * tt));
+            }
+            tt += h;
+        }
+        if (cycle % 5 == 0) mc.calc_u(mahi::util::seconds(t), state, control, traj);
+        control = mc.control_at_time(mahi::util::seconds(t)).u;
+        double xd[4];
+        if (mmpc_linearize_batch_host(lin, 1, state.data(), control.data(), nullptr, nullptr, xd) != MMPC_OK) return 3;
+        std::printf("%.6f,%.17g,%.17g,%.17g,%.17g,%.17g,%.17g,%d,%d\n", t, state[0], state[1], state[2], state[3],
+                    control[0], control[1], mc.last_status(), mc.last_iterations());
+        for (int i = 0; i < 4; i++) state[i] += xd[i] * h;
+        t += h;
+        cycle++;
+    }
+    mmpc_destroy(lin);
+    return 0;
+}

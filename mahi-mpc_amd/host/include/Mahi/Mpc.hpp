@@ -1,0 +1,4 @@
+#pragma once
+#include <Mahi/Mpc/ModelControl.hpp>
+#include <Mahi/Mpc/ModelGenerator.hpp>
+#include <Mahi/Mpc/ModelParameters.hpp>
