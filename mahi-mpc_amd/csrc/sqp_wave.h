@@ -195,10 +195,8 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
     }
     // stages >= N are structurally zero in the static-NMAX loops below
     for (int i = N * NX * NX + lane; i < NMAX * NX * NX; i += 64) sA[i] = 0.0;
-    for (int i = N * NX * NU + lane; i < NMAX * NX * NU; i += 64) {
-        sB[i] = 0.0;
-        sZ[i] = 0.0;
-    }
+    for (int i = N * NX * NU + lane; i < NMAX * NX * NU; i += 64) sB[i] = 0.0;
+    for (int i = N * NX + lane; i < NMAX * NX; i += 64) sE[i] = 0.0;
     __syncthreads();
     if (lane < NX) sX[lane] = p.x0[inst * NX + lane];  // x_0 pinned (ModelControl.cpp:144-145)
     if (lane < NU) sUp[lane] = p.u_prev[inst * NU + lane];
@@ -315,11 +313,27 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
         __syncthreads();
         MMPC_PHASE(2);
 
-        // ---- 3+4. fused backward sweep (no LDS round trips, no barriers inside) ----
-        //   lanes 0..15  (row 0): P_{i+1}[pa][pb] -> Z_i = B_i^T P_{i+1}, P_i = Q + A_i^T P_{i+1} A_i
-        //                         rows of P/T via quad_perm, columns via row_ror:4/8/12
-        //   lanes 16..19 (quad 4): adjoint lam_i = Q e_{i-1} + A_i^T lam_{i+1}
+        // ---- 3+4+5a. one backward sweep over the stages, j = NMAX-1 .. 0 ----
+        //   lanes 0..15  (row 0): P_{j+1}[pa][pb] -> P_j = Q + A_j^T P_{j+1} A_j, Z_{j-1} = B_{j-1}^T P_j
+        //                         (rows of P/T via quad_perm, columns via row_ror:4/8/12)
+        //   lanes 16..19 (quad 4): adjoint lam_j = Q e_{j-1} + A_j^T lam_{j+1}
+        //   all lanes           : lower half of the condensed Hessian row (stage si, input sr),
+        //                         t_j = t_{j+1} A_{j+1} + d_j Z_j[sr],  H_ij = t_j B_j   (d_j = [j == si])
+        // The serial P / lam chains are latency-bound; the Hessian row work fills their gaps.  Stages
+        // >= N are structurally zero (A = B = e = 0), so P_j = Q and lam_j = 0 there.  Z_j goes through
+        // LDS (lanes 0..7 write, every lane reads its row one step later; same-wave LDS order).
+        const int si = lane / NU, sr = lane - (lane / NU) * NU;  // Hessian row lane = (stage si, input sr)
+        const bool row_valid = lane < M;
+        double hrow[MMAX];
         double lmax;
+        const double Rr = sW[NX + sr], Rmr = sW[NX + NU + sr];
+        const double dterm = Rr * ((si + 1 < N) ? 2.0 : 1.0) + Rmr;
+        double wdiag[NU], woff[NU];
+#pragma unroll
+        for (int c = 0; c < NU; ++c) {
+            wdiag[c] = (c == sr) ? dterm : 0.0;
+            woff[c] = (c == sr) ? -Rr : 0.0;
+        }
         {
             const int pa = (lane >> 2) & 3, pb = lane & 3;
             // row index of the value each lane receives from row_ror:4s (s = 1,2,3)
@@ -327,75 +341,95 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
             const int c2 = (row_rot4_src<2>(lane) >> 2) & 3;
             const int c3 = (row_rot4_src<3>(lane) >> 2) & 3;
             const bool lam_lane = (lane >> 2) == 4;
-            double P = (pa == pb) ? sW[pa] : 0.0;  // P_N = Q
-            double lam = Qa * sE[(N - 1) * NX + qa];  // lam_N
-            if (lam_lane) sLam[N * NX + qa] = lam;
-            lmax = lam_lane ? fabs(lam) : 0.0;
-            const int zr = pa < NU ? pa : NU - 1;  // Z row handled by this lane (lanes pa < NU store it)
-            // per-lane operands of step i: column pb of A_i (for T), A_i[c][pa] (for P), B_i[c][zr] (for Z),
-            // column qa of A_i (for lam), e_{i-1}[qa]
-            struct Ops {
-                double aT[4], aP[4], bZ[4], aL[4], e;
-            };
-            auto load_ops = [&](int i, Ops& o) {
-                const double* Ai = sA + i * NX * NX;
-                const double* Bi = sB + i * NX * NU;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    o.aT[c] = Ai[c * NX + pb];
-                    o.aL[c] = Ai[c * NX + qa];
-                }
-                o.aP[0] = Ai[pa * NX + pa];
-                o.aP[1] = Ai[c1 * NX + pa];
-                o.aP[2] = Ai[c2 * NX + pa];
-                o.aP[3] = Ai[c3 * NX + pa];
-                o.bZ[0] = Bi[pa * NU + zr];
-                o.bZ[1] = Bi[c1 * NU + zr];
-                o.bZ[2] = Bi[c2 * NU + zr];
-                o.bZ[3] = Bi[c3 * NU + zr];
-                o.e = sE[(i >= 1 ? i - 1 : 0) * NX + qa];
-            };
-            Ops cur;
-            load_ops(N - 1, cur);
+            const bool z_lane = lane < 16 && pa < NU;
+            const int zr = pa < NU ? pa : NU - 1;
             const double pq = (pa == pb) ? sW[pa] : 0.0;
-            for (int i = N - 1; i >= 0; --i) {
-                Ops nxt;
-                load_ops(i >= 1 ? i - 1 : 0, nxt);
-                // column pb of P_{i+1}: own value is row pa, rotations give rows c1..c3
+            double P = pq;                                   // P_NMAX = Q
+            double lam = Qa * sE[(NMAX - 1) * NX + qa];      // lam_NMAX (e_j = 0 for j >= N)
+            if (lam_lane) sLam[NMAX * NX + qa] = lam;
+            lmax = lam_lane ? fabs(lam) : 0.0;
+            {   // Z_{NMAX-1} = B^T Q
+                const double* Bi = sB + (NMAX - 1) * NX * NU;
                 const double P1 = row_rot4<1>(P), P2 = row_rot4<2>(P), P3 = row_rot4<3>(P);
-                if (lane < 16 && pa < NU) {
-                    const double z = fma(cur.bZ[3], P3, fma(cur.bZ[2], P2, fma(cur.bZ[1], P1, cur.bZ[0] * P)));
-                    sZ[i * NU * NX + pa * NX + pb] = z;
+                const double z = fma(Bi[c3 * NU + zr], P3, fma(Bi[c2 * NU + zr], P2,
+                                     fma(Bi[c1 * NU + zr], P1, Bi[pa * NU + zr] * P)));
+                if (z_lane) sZ[(NMAX - 1) * NU * NX + pa * NX + pb] = z;
+            }
+            double t[NX] = {0.0, 0.0, 0.0, 0.0};
+            double dprev = 0.0;  // d_{j+1}
+#pragma unroll
+            for (int j = NMAX - 1; j >= 0; --j) {
+                int jj = j;
+                asm volatile("" : "+s"(jj));
+                const double dj = (si == jj) ? 1.0 : 0.0;
+                // (a) Hessian row, lower part
+                {
+                    const double2* zp = reinterpret_cast<const double2*>(sZ + j * NU * NX + sr * NX);
+                    const double2 z01 = zp[0], z23 = zp[1];
+                    const double zz[NX] = {z01.x, z01.y, z23.x, z23.y};
+                    if (j < NMAX - 1) {
+                        const double* A1 = sA + (j + 1) * NX * NX;
+                        double tn[NX];
+#pragma unroll
+                        for (int q = 0; q < NX; ++q)
+                            tn[q] = fma(dj, zz[q], fma(t[3], A1[3 * NX + q], fma(t[2], A1[2 * NX + q],
+                                                       fma(t[1], A1[1 * NX + q], t[0] * A1[0 * NX + q]))));
+#pragma unroll
+                        for (int q = 0; q < NX; ++q) t[q] = tn[q];
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < NX; ++q) t[q] = dj * zz[q];
+                    }
+                    const double* Bj = sB + j * NX * NU;
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {
+                        const double base = fma(dprev, woff[c], dj * wdiag[c]);
+                        hrow[j * NU + c] = fma(t[3], Bj[3 * NU + c],
+                                               fma(t[2], Bj[2 * NU + c], fma(t[1], Bj[1 * NU + c], fma(t[0], Bj[0 * NU + c], base))));
+                        MMPC_PIN(hrow[j * NU + c]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) MMPC_PIN(t[q]);
+                    dprev = dj;
                 }
-                // T = P_{i+1} A_i : row pa of P by quad broadcast
-                const double r0 = quad_bcast<0>(P), r1 = quad_bcast<1>(P), r2 = quad_bcast<2>(P), r3 = quad_bcast<3>(P);
-                const double T = fma(r0, cur.aT[0], r1 * cur.aT[1]) + fma(r2, cur.aT[2], r3 * cur.aT[3]);
-                // P_i = Q + A_i^T T : column pb of T by row rotations
-                const double T1 = row_rot4<1>(T), T2 = row_rot4<2>(T), T3 = row_rot4<3>(T);
-                P = pq + (fma(cur.aP[0], T, cur.aP[1] * T1) + fma(cur.aP[2], T2, cur.aP[3] * T3));
-                // adjoint (quad 4)
-                if (i >= 1) {
-                    const double l0 = quad_bcast<0>(lam), l1 = quad_bcast<1>(lam), l2 = quad_bcast<2>(lam),
-                                 l3 = quad_bcast<3>(lam);
-                    lam = fma(Qa, cur.e, fma(cur.aL[0], l0, cur.aL[1] * l1) + fma(cur.aL[2], l2, cur.aL[3] * l3));
-                    if (lam_lane) {
-                        sLam[i * NX + qa] = lam;
-                        lmax = fmax(lmax, fabs(lam));
+                // (b) P_j = Q + A_j^T (P_{j+1} A_j), lam_j
+                {
+                    const double* Ai = sA + j * NX * NX;
+                    double aT[4];
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) aT[c] = Ai[c * NX + pb];  // column pb (= qa) of A_j
+                    const double r0 = quad_bcast<0>(P), r1 = quad_bcast<1>(P), r2 = quad_bcast<2>(P), r3 = quad_bcast<3>(P);
+                    const double T = fma(r0, aT[0], r1 * aT[1]) + fma(r2, aT[2], r3 * aT[3]);
+                    const double T1 = row_rot4<1>(T), T2 = row_rot4<2>(T), T3 = row_rot4<3>(T);
+                    P = pq + (fma(Ai[pa * NX + pa], T, Ai[c1 * NX + pa] * T1) +
+                              fma(Ai[c2 * NX + pa], T2, Ai[c3 * NX + pa] * T3));
+                    if (j >= 1) {
+                        const double l0 = quad_bcast<0>(lam), l1 = quad_bcast<1>(lam), l2 = quad_bcast<2>(lam),
+                                     l3 = quad_bcast<3>(lam);
+                        lam = fma(Qa, sE[(j - 1) * NX + qa], fma(aT[0], l0, aT[1] * l1) + fma(aT[2], l2, aT[3] * l3));
+                        if (lam_lane) {
+                            sLam[j * NX + qa] = lam;
+                            lmax = fmax(lmax, fabs(lam));
+                        }
                     }
                 }
-                cur = nxt;
+                // (c) Z_{j-1} = B_{j-1}^T P_j for the next step's Hessian rows
+                if (j >= 1) {
+                    const double* Bi = sB + (j - 1) * NX * NU;
+                    const double P1 = row_rot4<1>(P), P2 = row_rot4<2>(P), P3 = row_rot4<3>(P);
+                    const double z = fma(Bi[c3 * NU + zr], P3, fma(Bi[c2 * NU + zr], P2,
+                                         fma(Bi[c1 * NU + zr], P1, Bi[pa * NU + zr] * P)));
+                    if (z_lane) sZ[(j - 1) * NU * NX + pa * NX + pb] = z;
+                }
             }
         }
         __syncthreads();
         MMPC_PHASE(4);
-        const int si = lane / NU, sr = lane - (lane / NU) * NU;  // Hessian row lane = (stage si, input sr)
-        const bool row_valid = lane < M;
         double g = 0.0;
         if (row_valid) {
             const double* ln = sLam + (si + 1) * NX;
 #pragma unroll
             for (int q = 0; q < NX; ++q) g = fma(sB[si * NX * NU + q * NU + sr], ln[q], g);
-            const double Rr = sW[NX + sr], Rmr = sW[NX + NU + sr];
             const double ui = sU[si * NU + sr];
             const double um = (si == 0) ? sUp[sr] : sU[(si - 1) * NU + sr];
             g = fma(Rr, ui - um, fma(Rmr, ui, g));
@@ -423,63 +457,16 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
         }
         MMPC_PHASE(3);
 
-        // ---- 5. condensed Hessian, one row per lane ----
-        // lower part (j <= si): t_j = t_{j+1} A_{j+1} + d_j z,  H_ij = t_j B_j   (t_j == 0 for j > si)
-        // upper part (j >  si): w_j = A_j v_{j-1},  H_ij = Z_j w_j,  v_j = w_j + d_j b  (w_j == 0 for j <= si)
-        // with d_j = [j == si]; the two parts never overlap, so they simply add (no selects).  The D^T R D + Rm
-        // band (ModelGenerator.cpp:216-221) rides on the same indicators: diagonal at d_j, sub/super
-        // diagonals at d_{j+1} (lower sweep) and d_{j-1} (upper sweep).
-        double hrow[MMAX];
+        // ---- 5b. condensed Hessian, upper part (j > si): w_j = A_j v_{j-1},  H_ij = Z_j w_j,
+        //      v_j = w_j + d_j b (w_j == 0 for j <= si).  The lower and upper parts never overlap, so they
+        //      simply add (no selects).  The D^T R D + Rm band (ModelGenerator.cpp:216-221) rides on the
+        //      same indicators: diagonal at d_j, sub/super diagonals at d_{j+1} (lower) and d_{j-1} (upper).
         {
-            double z[NX], bcol[NX];
+            double bcol[NX];
 #pragma unroll
-            for (int q = 0; q < NX; ++q) {
-                z[q] = row_valid ? sZ[si * NU * NX + sr * NX + q] : 0.0;
-                bcol[q] = row_valid ? sB[si * NX * NU + q * NU + sr] : 0.0;
-            }
-            const int srr = sr < NU ? sr : 0;
-            const double Rr = sW[NX + srr], Rmr = sW[NX + NU + srr];
-            const double dterm = Rr * ((si + 1 < N) ? 2.0 : 1.0) + Rmr;
-            double wdiag[NU], woff[NU];
-#pragma unroll
-            for (int c = 0; c < NU; ++c) {
-                wdiag[c] = (c == sr) ? dterm : 0.0;
-                woff[c] = (c == sr) ? -Rr : 0.0;
-            }
-            double t[NX] = {0.0, 0.0, 0.0, 0.0};
-            double dprev = 0.0;  // d_{j+1}
-#pragma unroll
-            for (int j = NMAX - 1; j >= 0; --j) {
-                int jj = j;
-                asm volatile("" : "+s"(jj));
-                const double dj = (si == jj) ? 1.0 : 0.0;
-                if (j < NMAX - 1) {
-                    const double* A1 = sA + (j + 1) * NX * NX;
-                    double tn[NX];
-#pragma unroll
-                    for (int q = 0; q < NX; ++q)
-                        tn[q] = fma(t[3], A1[3 * NX + q],
-                                    fma(t[2], A1[2 * NX + q], fma(t[1], A1[1 * NX + q], fma(t[0], A1[0 * NX + q], dj * z[q]))));
-#pragma unroll
-                    for (int q = 0; q < NX; ++q) t[q] = tn[q];
-                } else {
-#pragma unroll
-                    for (int q = 0; q < NX; ++q) t[q] = dj * z[q];
-                }
-                const double* Bj = sB + j * NX * NU;
-#pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    const double base = fma(dprev, woff[c], dj * wdiag[c]);
-                    hrow[j * NU + c] = fma(t[3], Bj[3 * NU + c],
-                                           fma(t[2], Bj[2 * NU + c], fma(t[1], Bj[1 * NU + c], fma(t[0], Bj[0 * NU + c], base))));
-                    MMPC_PIN(hrow[j * NU + c]);
-                }
-#pragma unroll
-                for (int q = 0; q < NX; ++q) MMPC_PIN(t[q]);
-                dprev = dj;
-            }
+            for (int q = 0; q < NX; ++q) bcol[q] = row_valid ? sB[si * NX * NU + q * NU + sr] : 0.0;
             double v[NX] = {0.0, 0.0, 0.0, 0.0};
-            dprev = 0.0;  // d_{j-1}
+            double dprev = 0.0;  // d_{j-1}
 #pragma unroll
             for (int j = 0; j < NMAX; ++j) {
                 int jj = j;
