@@ -32,6 +32,16 @@ sys.path.insert(0, os.path.join(REPO, "mahi-mpc_amd"))
 METRIC = "MPC solves/sec (whole node), nx=4 N=30 batch, at 1/2/4/8 MI355X"
 SEED = 20250213
 WEIGHTS = [10.0, 1.0, 5.0, 5.0, 5.0, 5.0, 0.01, 0.01]
+# SURVEY.md 8d cfg#3 (exo): Q = [10 x4, 1 x4], R = 1 x4, Rm = 0.01 x4
+WEIGHTS_EXO = [10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4
+CONFIGS = {
+    "cfg2": dict(model="two_link_arm", nx=4, nu=2, N=30, B=4096, weights=WEIGHTS, metric=METRIC,
+                 workload="cfg#2: 2-link arm nx=4 nu=2, N=30, h=2 ms, cold-start GN-SQP to ||grad||<=1e-8, ||g||<=1e-10"),
+    "cfg3": dict(model="exo_arm", nx=8, nu=4, N=50, B=65536, weights=WEIGHTS_EXO,
+                 metric="MPC solves/sec (whole node), exo nx=8 N=50 batch (SURVEY.md 8d cfg#3/#4)",
+                 workload="cfg#3: 4-DoF exo nx=8 nu=4 (build-defined parameters), N=50, h=2 ms, cold-start GN-SQP "
+                          "(Riccati KKT) to ||grad||<=1e-8, ||g||<=1e-10"),
+}
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector = FP64 matrix peak (AMD spec)
 HBM_PEAK_GBS = 8000.0
 
@@ -41,8 +51,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU (cfg#2: 4096)")
-    ap.add_argument("--horizon", type=int, default=30)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
+                    help="cfg2 = headline (BASELINE.json); cfg3 = exo workload of SURVEY.md 8d")
+    ap.add_argument("--batch", type=int, default=None, help="instances per GPU (cfg#2: 4096, cfg#3: 65536)")
+    ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
@@ -50,25 +62,26 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(N, h, target_s):
+def cpu_baseline(cfg, N, h, target_s):
     """Oracle (oracle/liboracle.so, the same GN-SQP in plain C + OpenMP) on a bounded sample."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as o
+    model = o.EXO if cfg["model"] == "exo_arm" else o.TWO_LINK
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
-    w = np.array(WEIGHTS)
-    n0 = 4 * threads
-    x0, up, tr = o.synth(SEED, 0, n0, N, h)
+    w = np.array(cfg["weights"])
+    n0 = 2 * threads
+    x0, up, tr = o.synth(SEED, 0, n0, N, h, model=model)
     t = time.perf_counter()
-    o.solve_batch(N, h, x0, up, tr, w, nthreads=threads)
+    o.solve_batch(N, h, x0, up, tr, w, nthreads=threads, model=model)
     dt = time.perf_counter() - t
     n = int(max(n0, min(200000, n0 * target_s / max(dt, 1e-6))))
-    x0, up, tr = o.synth(SEED, 0, n, N, h)
+    x0, up, tr = o.synth(SEED, 0, n, N, h, model=model)
     t = time.perf_counter()
-    r = o.solve_batch(N, h, x0, up, tr, w, nthreads=threads)
+    r = o.solve_batch(N, h, x0, up, tr, w, nthreads=threads, model=model)
     dt = time.perf_counter() - t
     return dict(value=n / dt, unit="solves/s", cores=threads, kind="port",
-                sample=f"first {n} cfg#2 instances (seed {SEED}), cold start, {dt:.1f} s wall, "
-                       f"{int((r['status'] == 0).sum())}/{n} converged, oracle dense GN-SQP, "
+                sample=f"first {n} {cfg['workload'].split(':')[0]} instances (seed {SEED}), cold start, {dt:.1f} s "
+                       f"wall, {int((r['status'] == 0).sum())}/{n} converged, oracle dense condensed GN-SQP, "
                        f"{threads} OpenMP threads")
 
 
@@ -86,19 +99,24 @@ def main():
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    B, N, h_us = args.batch, args.horizon, 2000
+    cfg = CONFIGS[args.config]
+    B = args.batch or cfg["B"]
+    N = args.horizon or cfg["N"]
+    nx, nu, h_us = cfg["nx"], cfg["nu"], 2000
     h = h_us * 1e-6
 
     tmpdir = tempfile.mkdtemp(prefix="mmpc_bench_")
-    path = mmpc.write_model_json(os.path.join(tmpdir, "nonlinear_double_pendulum.json"),
-                                 "nonlinear_double_pendulum", 4, 2, h_us, N)
+    path = mmpc.write_model_json(os.path.join(tmpdir, f"{cfg['model']}.json"), cfg["model"], nx, nu, h_us, N,
+                                 model=cfg["model"])
     solver = mmpc.Solver(path, device=local)
+    solver.reserve_workspace(B)
+    riccati = cfg["model"] != "two_link_arm" or N * nu > 64
     NV = solver.NV
     f64 = dict(dtype=torch.float64, device=dev)
-    x0 = torch.empty((B, 4), **f64)
-    up = torch.empty((B, 2), **f64)
-    tr = torch.empty((B, N, 4), **f64)
-    w = torch.tensor(WEIGHTS, **f64)
+    x0 = torch.empty((B, nx), **f64)
+    up = torch.empty((B, nu), **f64)
+    tr = torch.empty((B, N, nx), **f64)
+    w = torch.tensor(cfg["weights"], **f64)
     V = torch.zeros((B, NV), **f64)
     st = torch.empty(B, dtype=torch.int32, device=dev)
     it = torch.empty(B, dtype=torch.int32, device=dev)
@@ -136,23 +154,32 @@ def main():
     conv = int(mdist.sum_over_ranks(int((status == 0).sum()), device=dev))
     total = B * world * args.steps
     value = total / elapsed
-    # algorithmic flops of one launch = SURVEY.md 8(d) per-iteration figure x the SQP iterations the
-    # launch's instances actually took (unit of work = 1 solve = sum over its iterations)
-    survey_fl = float(iters.sum()) * mmpc.survey_flops_per_iteration(N)
-    achieved = survey_fl / (kern_ms * 1e-3) / 1e12
-    fl = mmpc.flops_per_iteration(N)
-    own_fl = float(iters.sum()) * fl["total"]
+    # algorithmic flops of one launch = per-iteration figure x the SQP iterations the launch's instances
+    # actually took (unit of work = 1 solve = sum over its iterations).  Condensed kernel: the SURVEY.md 8(d)
+    # figure.  Riccati kernel: its own algorithmic count -- 8(d)'s figure prices the condensed algorithm
+    # (9.3 MFLOP/iter at cfg#3) and would overstate the achieved rate ~45x (reported alongside).
+    survey_fl = float(iters.sum()) * mmpc.survey_flops_per_iteration(N, nx, nu)
+    if riccati:
+        fl = mmpc.riccati_flops_per_iteration(N, nx, nu)
+        own_fl = float(iters.sum()) * fl["total"]
+        achieved = own_fl / (kern_ms * 1e-3) / 1e12
+        kname = f"sqp_lane_kernel<{'ExoArm' if cfg['model'] == 'exo_arm' else 'TwoLinkArm'}>"
+    else:
+        fl = mmpc.flops_per_iteration(N)
+        own_fl = float(iters.sum()) * fl["total"]
+        achieved = survey_fl / (kern_ms * 1e-3) / 1e12
+        kname = f"sqp_wave_kernel<TwoLinkArm,{30 if 16 < N <= 30 else (16 if N <= 16 else 32)}>"
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("batch") == B and tj.get("horizon") == N:
+            if tj.get("batch") == B and tj.get("horizon") == N and tj.get("config", "cfg2") == args.config:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
     out = {
-        "metric": METRIC,
+        "metric": cfg["metric"],
         "value": value,
         "unit": "solves/s",
         "n_gpus": world,
@@ -163,22 +190,23 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: counter-based splitmix64 cfg#2 instances (SURVEY.md 8d), generated on device",
-        "config": {"workload": "cfg#2: 2-link arm nx=4 nu=2, N=30, h=2 ms, cold-start GN-SQP to "
-                               "||grad||<=1e-8, ||g||<=1e-10", "batch_per_gpu": B, "global_batch": B * world,
-                   "horizon": N, "parallelism": f"batch-shard x{world} (no data-path collective)"},
+        "data": f"synthetic: counter-based splitmix64 {args.config} instances (SURVEY.md 8d), generated on device",
+        "config": {"workload": cfg["workload"], "batch_per_gpu": B, "global_batch": B * world,
+                   "horizon": N, "kkt_solver": "riccati (lane per instance)" if riccati else "condensed (wave per instance)",
+                   "parallelism": f"batch-shard x{world} (no data-path collective)"},
         "converged": conv,
         "mean_sqp_iters": float(iters.mean()),
         "kernel_ms": kern_ms,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": "sqp_wave_kernel<TwoLinkArm,30>",
-                     "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N),
+                     "kernel": kname,
+                     "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N, nx, nu),
                      "flops_per_iter_kernel_own_count": fl["total"],
-                     "kernel_own_count_tflops": own_fl / (kern_ms * 1e-3) / 1e12},
+                     "kernel_own_count_tflops": own_fl / (kern_ms * 1e-3) / 1e12,
+                     "survey_8d_equivalent_tflops": survey_fl / (kern_ms * 1e-3) / 1e12},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(N, h, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
     solver.close()

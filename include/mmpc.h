@@ -35,15 +35,19 @@
  *     ModelControl.cpp:29-50) and the solution on exit.  V[b][0:nx] is pinned to x0[b]
  *     as the reference pins x_0 through lbx = ubx = state (ModelControl.cpp:144-145).
  *   - mmpc_solve_batch takes DEVICE pointers and is stream-ordered on `stream`
- *     (a hipStream_t; NULL = default stream).  It never allocates and never
- *     synchronises.  mmpc_solve_batch_host takes host pointers and is synchronous.
+ *     (a hipStream_t; NULL = default stream) and never synchronises.  The condensed
+ *     solver never allocates; the Riccati solver uses a per-handle device workspace
+ *     that grows (synchronously) when a larger B arrives -- call
+ *     mmpc_reserve_workspace first to keep solves allocation-free (hipGraph capture).
+ *     mmpc_solve_batch_host takes host pointers and is synchronous.
  *   - Functions return MMPC_OK (0) or a negative mmpc_result and never throw.
  *     Non-convergence is NOT an API error: it is reported per instance in
  *     status[] (the reference silently uses non-converged IPOPT output,
  *     ModelControl.cpp:159-163; callers here can see it).
  *   - A handle may be used from several threads only on distinct streams and only
- *     for the device-pointer entry points; the _host entry points serialise on an
- *     internal mutex.
+ *     for the device-pointer entry points of the condensed solver (the Riccati
+ *     workspace is per handle: use one handle per concurrent stream); the _host
+ *     entry points serialise on an internal mutex.
  */
 #ifndef MMPC_H
 #define MMPC_H
@@ -54,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MMPC_ABI_VERSION 1
+#define MMPC_ABI_VERSION 2
 
 typedef struct mmpc_handle mmpc_handle;
 
@@ -82,7 +86,16 @@ enum mmpc_status {
 
 /* built-in dynamics (device code; see DESIGN.md "Models") */
 enum mmpc_model_id {
-    MMPC_MODEL_TWO_LINK_ARM = 0 /* examples/ex_model_generate.cpp:24-43, nx=4 nu=2 */
+    MMPC_MODEL_TWO_LINK_ARM = 0, /* examples/ex_model_generate.cpp:24-43, nx=4 nu=2 */
+    MMPC_MODEL_EXO_ARM = 1       /* 4-DoF exo, nx=8 nu=4: M(q) of src/inverseTest.cpp:59-74 with the
+                                    build-defined parameters of tests/golden/exo_params.json */
+};
+
+/* KKT solve of each SQP iteration (both solve the same Gauss-Newton QP exactly) */
+enum mmpc_kkt_solver {
+    MMPC_KKT_AUTO = 0,      /* condensed when N*nu <= 64 and the model is the 2-link arm, else Riccati */
+    MMPC_KKT_CONDENSED = 1, /* one wavefront per instance, condensed Hessian row per lane (N*nu <= 64) */
+    MMPC_KKT_RICCATI = 2    /* one lane per instance, Riccati recursion, any N (needs a workspace) */
 };
 
 typedef struct mmpc_opts {
@@ -90,6 +103,8 @@ typedef struct mmpc_opts {
     int32_t device;     /* HIP device ordinal; -1 = the calling thread's current device. default -1 */
     double tol_grad;    /* ||grad_u J_reduced||_inf stop tolerance. default 1e-8 */
     double tol_defect;  /* ||g||_inf stop tolerance. default 1e-10 */
+    int32_t kkt_solver; /* enum mmpc_kkt_solver. default MMPC_KKT_AUTO */
+    int32_t reserved;
 } mmpc_opts;
 
 typedef struct mmpc_model_info {
@@ -115,6 +130,9 @@ int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_han
 int mmpc_destroy(mmpc_handle* h);
 int mmpc_get_model_info(const mmpc_handle* h, mmpc_model_info* info);
 int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts);
+/* Pre-allocate the Riccati solver's device workspace for batches up to B (no-op for the
+ * condensed solver).  *bytes (may be NULL) receives the workspace size. */
+int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes);
 
 /* Batched SQP solve, DEVICE pointers, stream-ordered.  u_lb/u_ub: device [nu] or NULL
  * (unbounded; |bound| >= 1e19 is unbounded as in IPOPT).  status/iters/kkt_res: device
@@ -142,8 +160,9 @@ int mmpc_nlp_eval_batch(mmpc_handle* h, int64_t B, const double* V, const double
                         const double* traj, const double* weights, int64_t weights_stride,
                         double* J, double* defect_inf, void* stream);
 
-/* Synthetic cfg#2 instances: counter-based splitmix64(seed, first_index + b),
- * so shards generate identical instances whatever the GPU count.  DEVICE pointers. */
+/* Synthetic instances: cfg#2 recipe for the 2-link arm, cfg#3 recipe for the exo;
+ * counter-based splitmix64(seed, first_index + b), so shards generate identical instances
+ * whatever the GPU count.  DEVICE pointers. */
 int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t B, double* x0,
                      double* u_prev, double* traj, void* stream);
 

@@ -91,6 +91,31 @@ MMPC_HD Dual<K> operator-(const Dual<K>& a, double s) {
     return r;
 }
 template <int K>
+MMPC_HD Dual<K> operator+(double s, const Dual<K>& a) {
+    return a + s;
+}
+template <int K>
+MMPC_HD Dual<K> operator-(double s, const Dual<K>& a) {
+    Dual<K> r;
+    r.v = s - a.v;
+#pragma unroll
+    for (int i = 0; i < K; ++i) r.d[i] = -a.d[i];
+    return r;
+}
+// a constant of the scalar type (generated model code)
+template <class T>
+struct Lift {
+    static MMPC_HD T from(double c) { return c; }
+};
+template <int K>
+struct Lift<Dual<K>> {
+    static MMPC_HD Dual<K> from(double c) { return dual_const<K>(c); }
+};
+template <class T>
+MMPC_HD T lift(double c) {
+    return Lift<T>::from(c);
+}
+template <int K>
 MMPC_HD Dual<K> operator/(const Dual<K>& a, const Dual<K>& b) {
     Dual<K> r;
     const double ib = 1.0 / b.v;

@@ -19,6 +19,7 @@
 #include "../../include/mmpc.h"
 #include "json_lite.h"
 #include "models.h"
+#include "sqp_lane.h"
 #include "sqp_wave.h"
 
 using namespace mmpc;
@@ -51,6 +52,11 @@ struct mmpc_handle {
     // device staging for the *_host entry points (grown on demand)
     double* d_buf = nullptr;
     size_t d_buf_bytes = 0;
+    // Riccati solver workspace (SoA, sqp_lane.h LaneLayout), grown on demand
+    std::mutex ws_mu;
+    double* ws = nullptr;
+    size_t ws_bytes = 0;
+    int ws_dev = -1;
 };
 
 namespace {
@@ -140,20 +146,27 @@ int parse_model(const std::string& text, mmpc_model_info* info) {
     const json::Value* mdl = m->get("mmpc_model");
     if (mdl && mdl->kind == json::Value::String) {
         if (mdl->str == "two_link_arm" || mdl->str == "double_pendulum") info->model_id = MMPC_MODEL_TWO_LINK_ARM;
+        else if (mdl->str == "exo_arm" || mdl->str == "exo") info->model_id = MMPC_MODEL_EXO_ARM;
         else return fail(MMPC_ERR_UNSUPPORTED, "unknown mmpc_model \"" + mdl->str + "\"");
     } else if (info->num_x == 4 && info->num_u == 2) {
         info->model_id = MMPC_MODEL_TWO_LINK_ARM;
+    } else if (info->num_x == 8 && info->num_u == 4) {
+        info->model_id = MMPC_MODEL_EXO_ARM;
     } else {
         return fail(MMPC_ERR_UNSUPPORTED, "no built-in dynamics for these dimensions (set \"mmpc_model\")");
     }
     if (info->model_id == MMPC_MODEL_TWO_LINK_ARM && (info->num_x != 4 || info->num_u != 2))
         return fail(MMPC_ERR_PARSE, "two_link_arm needs num_x = 4, num_u = 2");
+    if (info->model_id == MMPC_MODEL_EXO_ARM && (info->num_x != 8 || info->num_u != 4))
+        return fail(MMPC_ERR_PARSE, "exo_arm needs num_x = 8, num_u = 4");
     return MMPC_OK;
 }
 
 int validate_opts(const mmpc_opts* o) {
     if (o->max_iter < 0 || o->max_iter > 100000) return fail(MMPC_ERR_INVALID_ARG, "max_iter out of range");
     if (!(o->tol_grad > 0.0) || !(o->tol_defect > 0.0)) return fail(MMPC_ERR_INVALID_ARG, "tolerances must be > 0");
+    if (o->kkt_solver < MMPC_KKT_AUTO || o->kkt_solver > MMPC_KKT_RICCATI)
+        return fail(MMPC_ERR_INVALID_ARG, "unknown kkt_solver");
     return MMPC_OK;
 }
 
@@ -295,7 +308,65 @@ __global__ __launch_bounds__(256) void synth_two_link_kernel(uint64_t seed, int6
     }
 }
 
+// SURVEY.md 8d cfg#3 instance generator (identical recipe in oracle/mmpc_oracle.c): q, qd ~ U[-0.5, 0.5],
+// tau_prev ~ U[-1, 1], per joint a ~ U[0.1, 0.4], f ~ U[0.25, 1] Hz, phase ~ U[0, 2 pi];
+// r_k = [a sin(2 pi f t_k + phase); 2 pi f a cos(2 pi f t_k + phase)], t_k = k h.
+__device__ __forceinline__ double unit_draw_exo(uint64_t seed, int64_t index, int j) {
+    const uint64_t v = splitmix64((seed + 0x3C6EF372FE94F82Aull) ^ splitmix64((uint64_t)index * 32ull + (uint64_t)j));
+    return (double)(v >> 11) * 0x1.0p-53;
+}
+__global__ __launch_bounds__(256) void synth_exo_kernel(uint64_t seed, int64_t first, int64_t B, int N, double h,
+                                                        double* x0, double* u_prev, double* traj) {
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const double PI = 3.14159265358979323846;
+    const int64_t gi = first + b;
+    double a[4], f[4], ph[4];
+    for (int j = 0; j < 4; ++j) {
+        x0[b * 8 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, j));
+        x0[b * 8 + 4 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, 4 + j));
+        u_prev[b * 4 + j] = affine_draw(-1.0, 2.0, unit_draw_exo(seed, gi, 8 + j));
+        a[j] = affine_draw(0.1, 0.3, unit_draw_exo(seed, gi, 12 + j));
+        f[j] = affine_draw(0.25, 0.75, unit_draw_exo(seed, gi, 16 + j));
+        ph[j] = affine_draw(0.0, 2.0 * PI, unit_draw_exo(seed, gi, 20 + j));
+    }
+    for (int k = 0; k < N; ++k) {
+        double* r = traj + (b * N + k) * 8;
+        for (int j = 0; j < 4; ++j) {
+            const double arg = 2.0 * PI * f[j] * (k * h) + ph[j];
+            r[j] = a[j] * sin(arg);
+            r[4 + j] = 2.0 * PI * f[j] * a[j] * cos(arg);
+        }
+    }
+}
+
 inline unsigned grid1d(int64_t B, int threads) { return static_cast<unsigned>((B + threads - 1) / threads); }
+
+size_t workspace_bytes(const mmpc_model_info& mi, int64_t B) {
+    const int64_t blocks = (B + 63) / 64;
+    return static_cast<size_t>(lane_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) * 64u *
+           static_cast<size_t>(blocks) * sizeof(double);
+}
+
+// Riccati workspace for B instances (SoA per 64-instance block, sqp_lane.h).  Growth is synchronous:
+// hipFree waits for the kernels still using the old buffer.
+int ensure_workspace(mmpc_handle* h, int64_t B, LaneWork* lw) {
+    const size_t bytes = workspace_bytes(h->info, B);
+    int dev = -1;
+    MMPC_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(h->ws_mu);
+    if (h->ws && h->ws_dev != dev) return fail(MMPC_ERR_INVALID_ARG, "handle used on two devices");
+    if (bytes > h->ws_bytes) {
+        if (h->ws) MMPC_HIP(hipFree(h->ws));
+        h->ws = nullptr;
+        h->ws_bytes = 0;
+        MMPC_HIP(hipMalloc(reinterpret_cast<void**>(&h->ws), bytes));
+        h->ws_bytes = bytes;
+        h->ws_dev = dev;
+    }
+    lw->ws = h->ws;
+    return MMPC_OK;
+}
 
 int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
                  const double* weights, int64_t w_stride, const double* u_lb, const double* u_ub, double* V,
@@ -327,15 +398,26 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.iters = iters;
     p.kkt = kkt;
     p.trace = trace;
-    if (mi.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "model not built in");
-    // host-side shape checks: the kernel holds one condensed-Hessian row per lane
     const int N = mi.num_shooting_nodes;
-    if (N * TwoLinkArm::NU > 64)
-        return fail(MMPC_ERR_UNSUPPORTED, "N*nu > 64: horizon too long for the single-wave kernel");
-    dim3 grid(static_cast<unsigned>(B)), block(64);
-    if (N <= 16) sqp_wave_kernel<TwoLinkArm, 16><<<grid, block, 0, stream>>>(p);
-    else if (N <= 30) sqp_wave_kernel<TwoLinkArm, 30><<<grid, block, 0, stream>>>(p);
-    else sqp_wave_kernel<TwoLinkArm, 32><<<grid, block, 0, stream>>>(p);
+    int solver = h->opts.kkt_solver;
+    const bool condensed_ok = mi.model_id == MMPC_MODEL_TWO_LINK_ARM && N * TwoLinkArm::NU <= 64;
+    if (solver == MMPC_KKT_AUTO) solver = condensed_ok ? MMPC_KKT_CONDENSED : MMPC_KKT_RICCATI;
+    if (solver == MMPC_KKT_CONDENSED) {
+        // host-side shape checks: the kernel holds one condensed-Hessian row per lane
+        if (!condensed_ok)
+            return fail(MMPC_ERR_UNSUPPORTED, "condensed solver needs the 2-link arm and N*nu <= 64");
+        dim3 grid(static_cast<unsigned>(B)), block(64);
+        if (N <= 16) sqp_wave_kernel<TwoLinkArm, 16><<<grid, block, 0, stream>>>(p);
+        else if (N <= 30) sqp_wave_kernel<TwoLinkArm, 30><<<grid, block, 0, stream>>>(p);
+        else sqp_wave_kernel<TwoLinkArm, 32><<<grid, block, 0, stream>>>(p);
+    } else {
+        LaneWork lw;
+        int rc = ensure_workspace(h, B, &lw);
+        if (rc) return rc;
+        dim3 grid(grid1d(B, 64)), block(64);
+        if (mi.model_id == MMPC_MODEL_EXO_ARM) sqp_lane_kernel<ExoArm><<<grid, block, 0, stream>>>(p, lw);
+        else sqp_lane_kernel<TwoLinkArm><<<grid, block, 0, stream>>>(p, lw);
+    }
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
 }
@@ -372,6 +454,8 @@ void mmpc_default_opts(mmpc_opts* o) {
     o->device = -1;
     o->tol_grad = 1e-8;
     o->tol_defect = 1e-10;
+    o->kkt_solver = MMPC_KKT_AUTO;
+    o->reserved = 0;
 }
 
 int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_handle** out) {
@@ -410,6 +494,10 @@ int mmpc_destroy(mmpc_handle* h) {
         if (h->d_buf) (void)hipFree(h->d_buf);
         if (h->host_stream) (void)hipStreamDestroy(h->host_stream);
     }
+    if (h->ws) {
+        DeviceGuard g(h->ws_dev);
+        (void)hipFree(h->ws);
+    }
     delete h;
     return MMPC_OK;
 }
@@ -426,6 +514,21 @@ int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts) {
     if (rc) return rc;
     h->opts = *opts;
     return MMPC_OK;
+}
+
+int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    const size_t nb = workspace_bytes(h->info, B);
+    if (bytes) *bytes = nb;
+    if (B == 0) return MMPC_OK;
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    LaneWork lw;
+    return ensure_workspace(h, B, &lw);
 }
 
 int mmpc_solve_batch(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
@@ -495,14 +598,17 @@ int mmpc_linearize_batch(mmpc_handle* h, int64_t B, const double* x, const doubl
     if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
     if (B == 0) return MMPC_OK;
     if (!x || !u) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
-    if (h->info.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "model not built in");
     int dev;
     int rc = resolve_device(h, &dev);
     if (rc) return rc;
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
-    linearize_kernel<TwoLinkArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        B, x, u, A_colmajor, B_colmajor, xdot);
+    if (h->info.model_id == MMPC_MODEL_EXO_ARM)
+        linearize_kernel<ExoArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            B, x, u, A_colmajor, B_colmajor, xdot);
+    else
+        linearize_kernel<TwoLinkArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            B, x, u, A_colmajor, B_colmajor, xdot);
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
 }
@@ -543,15 +649,19 @@ int mmpc_nlp_eval_batch(mmpc_handle* h, int64_t B, const double* V, const double
     if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
     if (B == 0) return MMPC_OK;
     if (!V || !u_prev || !traj || !weights) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
-    if (h->info.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "model not built in");
     int dev;
     int rc = resolve_device(h, &dev);
     if (rc) return rc;
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
-    nlp_eval_kernel<TwoLinkArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
-        weights_stride, J, defect_inf);
+    if (h->info.model_id == MMPC_MODEL_EXO_ARM)
+        nlp_eval_kernel<ExoArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
+            weights_stride, J, defect_inf);
+    else
+        nlp_eval_kernel<TwoLinkArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
+            weights_stride, J, defect_inf);
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
 }
@@ -562,14 +672,17 @@ int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t
     if (B < 0 || first_index < 0) return fail(MMPC_ERR_INVALID_ARG, "negative B / first_index");
     if (B == 0) return MMPC_OK;
     if (!x0 || !u_prev || !traj) return fail(MMPC_ERR_INVALID_ARG, "null output pointer");
-    if (h->info.model_id != MMPC_MODEL_TWO_LINK_ARM) return fail(MMPC_ERR_UNSUPPORTED, "generator is cfg#2 only");
     int dev;
     int rc = resolve_device(h, &dev);
     if (rc) return rc;
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
-    synth_two_link_kernel<<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
+    if (h->info.model_id == MMPC_MODEL_EXO_ARM)
+        synth_exo_kernel<<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
+    else
+        synth_two_link_kernel<<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
 }

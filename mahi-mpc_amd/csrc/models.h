@@ -6,6 +6,7 @@
 // the scalar type (double or Dual<NX+NU>), compiled into the solver kernel.
 #pragma once
 #include "dual.h"
+#include "exo_model_gen.h"
 
 namespace mmpc {
 
@@ -38,11 +39,18 @@ struct TwoLinkArm {
         xd[2] = -(nA * inv_den);
         xd[3] = nB * inv_den;
     }
+    static constexpr int NQ = 2;  // second-order: x = [q; qd], xdot = [qd; acc(x, u)]
+    MMPC_HD static void eval(const double* x, const double* u, double* xd) { xdot<double>(x, u, xd); }
+    MMPC_HD static void eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu);
+    // acceleration and its partials d acc/dq [NQ*NQ], d acc/dqd [NQ*NQ], d acc/du [NQ*NU] (row-major)
+    MMPC_HD static void eval_acc_jac(const double* x, const double* u, double* acc, double* Fq, double* Fqd,
+                                     double* Fu);
 };
 
-// Values and continuous-time Jacobians of any model: fx[NX*NX], fu[NX*NU] row-major.
+// Forward-mode Jacobian of a model written as a scalar template: values and the continuous-time
+// Jacobians fx[NX*NX], fu[NX*NU] row-major.
 template <class Model>
-MMPC_HD void model_eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
+MMPC_HD void dual_eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
     constexpr int NX = Model::NX, NU = Model::NU, K = NX + NU;
     Dual<K> xv[NX], uv[NU], xdv[NX];
 #pragma unroll
@@ -60,9 +68,174 @@ MMPC_HD void model_eval_jac(const double* x, const double* u, double* xd, double
     }
 }
 
+// 4-DoF forearm/wrist exo, state [q0..q3, qd0..qd3] (util/testCorrectEquations.py:16-23),
+// control tau[4].  xdot = [qd; M(q)^-1 (tau - D qd - G(q))] with M(q) of src/inverseTest.cpp:59-74
+// (generated, exo_model_gen.h) and the build-defined gravity G_i = g_i sin q_i and viscous damping D of
+// tests/golden/exo_params.json -- the reference defines neither, so these are NOT reference-pinned.
+// M^-1 is applied through a 4x4 Cholesky factor; the Jacobian is analytic:
+//   d qdd / dq_j   = M^-1 (-dM/dq_j qdd - dG/dq_j e_j),  d qdd / dqd = -M^-1 D,  d qdd / dtau = M^-1,
+// with dM/dq_j from the generated symbolic-derivative polynomials.
+struct ExoArm {
+    static constexpr int NX = 8;
+    static constexpr int NU = 4;
+    static constexpr int NQ = 4;  // second-order: x = [q; qd], xdot = [qd; acc(x, u)]
+
+    // Cholesky of the upper-packed SPD matrix a (M00 M01 M02 M03 M11 M12 M13 M22 M23 M33):
+    // l = lower factor packed (L00 L10 L11 L20 L21 L22 L30 L31 L32 L33), il = 1 / diag
+    MMPC_HD static void chol4(const double* a, double* l, double* il) {
+        l[0] = sqrt(a[0]);
+        il[0] = 1.0 / l[0];
+        l[1] = a[1] * il[0];
+        l[3] = a[2] * il[0];
+        l[6] = a[3] * il[0];
+        l[2] = sqrt(a[4] - l[1] * l[1]);
+        il[1] = 1.0 / l[2];
+        l[4] = (a[5] - l[3] * l[1]) * il[1];
+        l[7] = (a[6] - l[6] * l[1]) * il[1];
+        l[5] = sqrt(a[7] - l[3] * l[3] - l[4] * l[4]);
+        il[2] = 1.0 / l[5];
+        l[8] = (a[8] - l[6] * l[3] - l[7] * l[4]) * il[2];
+        l[9] = sqrt(a[9] - l[6] * l[6] - l[7] * l[7] - l[8] * l[8]);
+        il[3] = 1.0 / l[9];
+    }
+    // y = (L L^T)^-1 b
+    MMPC_HD static void chol4_solve(const double* l, const double* il, const double* b, double* y) {
+        const double z0 = b[0] * il[0];
+        const double z1 = (b[1] - l[1] * z0) * il[1];
+        const double z2 = (b[2] - l[3] * z0 - l[4] * z1) * il[2];
+        const double z3 = (b[3] - l[6] * z0 - l[7] * z1 - l[8] * z2) * il[3];
+        y[3] = z3 * il[3];
+        y[2] = (z2 - l[8] * y[3]) * il[2];
+        y[1] = (z1 - l[4] * y[2] - l[7] * y[3]) * il[1];
+        y[0] = (z0 - l[1] * y[1] - l[3] * y[2] - l[6] * y[3]) * il[0];
+    }
+
+    MMPC_HD static void eval(const double* x, const double* u, double* xd) {
+        double s[4], c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sincos(x[i], &s[i], &c[i]);
+        const exo::TrigPowers tp(c[1], c[2], c[3], s[1], s[2], s[3]);
+        double Mu[10];
+        exo::mass_upper(tp, Mu);
+        double l[10], il[4], w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = u[i] - exo::kDamping[i] * x[4 + i] - exo::kGravityGain[i] * s[i];
+        chol4(Mu, l, il);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xd[i] = x[4 + i];
+        chol4_solve(l, il, w, xd + 4);
+    }
+
+    // (dM/dq_J) v for the upper-packed symmetric dM/dq_J
+    template <int J>
+    MMPC_HD static void dmass_times(const exo::TrigPowers& tp, const double* v, double* out) {
+        double dM[10];
+        exo::dmass_upper<J>(tp, dM);
+        out[0] = fma(dM[0], v[0], fma(dM[1], v[1], fma(dM[2], v[2], dM[3] * v[3])));
+        out[1] = fma(dM[1], v[0], fma(dM[4], v[1], fma(dM[5], v[2], dM[6] * v[3])));
+        out[2] = fma(dM[2], v[0], fma(dM[5], v[1], fma(dM[7], v[2], dM[8] * v[3])));
+        out[3] = fma(dM[3], v[0], fma(dM[6], v[1], fma(dM[8], v[2], dM[9] * v[3])));
+    }
+
+    // acceleration and its partials d qdd/dq [4x4], d qdd/dqd [4x4], d qdd/dtau [4x4] (row-major)
+    MMPC_HD static void eval_acc_jac(const double* x, const double* u, double* qdd, double* Fq, double* Fqd,
+                                     double* Fu) {
+        double s[4], c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sincos(x[i], &s[i], &c[i]);
+        const exo::TrigPowers tp(c[1], c[2], c[3], s[1], s[2], s[3]);
+        double Mu[10], l[10], il[4], w[4];
+        exo::mass_upper(tp, Mu);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = u[i] - exo::kDamping[i] * x[4 + i] - exo::kGravityGain[i] * s[i];
+        chol4(Mu, l, il);
+        chol4_solve(l, il, w, qdd);
+        // M^-1 (symmetric) = d qdd/dtau
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            double e[4] = {0.0, 0.0, 0.0, 0.0}, col[4];
+            e[j] = 1.0;
+            chol4_solve(l, il, e, col);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Fu[r * 4 + j] = col[r];
+        }
+        // d qdd/dq_j = M^-1 (-(dM/dq_j) qdd - g_j cos q_j e_j);  d qdd/dqd_j = -M^-1 e_j D_j
+        double rhs[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rhs[0][r] = 0.0;
+        dmass_times<1>(tp, qdd, rhs[1]);
+        dmass_times<2>(tp, qdd, rhs[2]);
+        dmass_times<3>(tp, qdd, rhs[3]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rhs[j][r] = -rhs[j][r];
+            rhs[j][j] -= exo::kGravityGain[j] * c[j];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                double t = 0.0;
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) t = fma(Fu[r * 4 + cc], rhs[j][cc], t);
+                Fq[r * 4 + j] = t;
+                Fqd[r * 4 + j] = -Fu[r * 4 + j] * exo::kDamping[j];
+            }
+        }
+    }
+
+    MMPC_HD static void eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
+        double qdd[4], Fq[16], Fqd[16], Fu[16];
+        eval_acc_jac(x, u, qdd, Fq, Fqd, Fu);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            xd[r] = x[4 + r];
+            xd[4 + r] = qdd[r];
+#pragma unroll
+            for (int cc = 0; cc < 8; ++cc) fx[r * 8 + cc] = (cc == 4 + r) ? 1.0 : 0.0;
+#pragma unroll
+            for (int cc = 0; cc < 4; ++cc) {
+                fx[(4 + r) * 8 + cc] = Fq[r * 4 + cc];
+                fx[(4 + r) * 8 + 4 + cc] = Fqd[r * 4 + cc];
+                fu[r * 4 + cc] = 0.0;
+                fu[(4 + r) * 4 + cc] = Fu[r * 4 + cc];
+            }
+        }
+    }
+};
+
+MMPC_HD void TwoLinkArm::eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
+    dual_eval_jac<TwoLinkArm>(x, u, xd, fx, fu);
+}
+MMPC_HD void TwoLinkArm::eval_acc_jac(const double* x, const double* u, double* acc, double* Fq, double* Fqd,
+                                      double* Fu) {
+    constexpr int K = NX + NU;
+    Dual<K> xv[NX], uv[NU], xdv[NX];
+#pragma unroll
+    for (int i = 0; i < NX; ++i) xv[i] = dual_var<K>(x[i], i);
+#pragma unroll
+    for (int i = 0; i < NU; ++i) uv[i] = dual_var<K>(u[i], NX + i);
+    xdot<Dual<K>>(xv, uv, xdv);
+#pragma unroll
+    for (int r = 0; r < NQ; ++r) {
+        acc[r] = xdv[NQ + r].v;
+#pragma unroll
+        for (int c = 0; c < NQ; ++c) {
+            Fq[r * NQ + c] = xdv[NQ + r].d[c];
+            Fqd[r * NQ + c] = xdv[NQ + r].d[NQ + c];
+        }
+#pragma unroll
+        for (int c = 0; c < NU; ++c) Fu[r * NU + c] = xdv[NQ + r].d[NX + c];
+    }
+}
+
+// Values and continuous-time Jacobians of any model: fx[NX*NX], fu[NX*NU] row-major.
+template <class Model>
+MMPC_HD void model_eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
+    Model::eval_jac(x, u, xd, fx, fu);
+}
+
 template <class Model>
 MMPC_HD void model_eval(const double* x, const double* u, double* xd) {
-    Model::template xdot<double>(x, u, xd);
+    Model::eval(x, u, xd);
 }
 
 }  // namespace mmpc

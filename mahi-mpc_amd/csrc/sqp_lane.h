@@ -1,0 +1,660 @@
+// sqp_lane.h -- batched GN-SQP with a Riccati KKT solve, ONE INSTANCE PER LANE.
+//
+// The wave kernel (sqp_wave.h) condenses the QP into an (N nu)x(N nu) Hessian held one row per lane,
+// which caps N nu at 64.  The exo configurations (SURVEY.md 8d cfg#3-#5: nx=8, nu=4, N=50, B=65536)
+// have N nu = 200: a condensed Hessian would be 320 KB per instance (2x the LDS of a CU) and
+// 9.3 MFLOP per iteration.  The same QP is solved exactly by a Riccati recursion on the augmented
+// state s_k = [dx_k; du_{k-1}] (the du_{k-1} block carries the Delta-u weight R of
+// ModelGenerator.cpp:216-221) in ~0.25 MFLOP per iteration, and at B = 65536 one instance per lane
+// already fills every SIMD of the MI355X (1024 waves), so lanes never exchange data.
+//
+// Per SQP iteration, per lane (all fp64; the NLP, merit, line search and stopping test are those of
+// sqp_wave.h and oracle/mmpc_oracle.c):
+//   (1) forward  : F_k, A_k = I + h f_x, B_k = h f_u, defects c_k, d_{k+1} = A_k d_k + c_k, merit J, |c|_1
+//   (2) backward : adjoint lam_k and reduced gradient g_k (stopping test), Riccati
+//                  H_ww = B^T G + P_ux B + P_uu + R + Rm,  G = P_xx B + P_xu,  H_wx = G^T A,
+//                  H_xx = A^T P_xx A,  K_k = -H_ww^-1 [H_wx | -R],  P_k = blkdiag(H_xx, R) - ...
+//   (3) forward  : du_k = K_k s_k + kff_k, dx_{k+1} = A_k dx_k + B_k du_k + c_k, directional derivative
+//   (4) l1-merit Armijo line search (value-only model evaluations)
+// A_k, B_k are recomputed in (2) and (3) instead of stored: one Jacobian evaluation costs ~1k FMA
+// while storing them would add 2x768 B of HBM traffic per stage and lane (DESIGN.md "Riccati path").
+// Per-lane state lives in a structure-of-arrays workspace in HBM ([wave block][element][lane]), so every
+// wave access is one contiguous 512-byte line.
+#pragma once
+#include "models.h"
+#include "sqp_wave.h"
+
+namespace mmpc {
+
+// Workspace layout, stage-major: [64-instance block][stage k = 0..N+1][field][lane].  All fields of
+// stage k sit at compile-time offsets from one wave-uniform base, so an access is base(k) + const in
+// scalar registers plus the lane offset in one VGPR (an [element][lane] layout hoists one 64-bit
+// per-lane pointer per (field, element) and spills).  Stage N holds x_N, d_N, dx_N; stage N+1 holds
+// the linear-mode data; stage N+2 is per-lane scratch for the Riccati step (W = P_xx A).
+__host__ __device__ constexpr int lane_stage_stride(int nx, int nu) { return 5 * nx + 2 * nu + nu * (nx + nu + 1); }
+__host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int N) { return (N + 3) * lane_stage_stride(nx, nu); }
+template <int NX, int NU>
+struct StageFields {
+    static constexpr int NS = NX + NU;
+    static constexpr int X = 0;             // x_k
+    static constexpr int U = X + NX;        // u_k
+    static constexpr int R = U + NU;        // r_k (target of F(x_k, u_k))
+    static constexpr int C = R + NX;        // defect c_k = F_k - x_{k+1}
+    static constexpr int D = C + NX;        // d_k (defect propagation)
+    static constexpr int DX = D + NX;       // dx_k
+    static constexpr int DU = DX + NX;      // du_k
+    static constexpr int K = DU + NU;       // [K_k | kff_k], nu x (nx+nu+1)
+    static constexpr int SS = K + NU * (NS + 1);
+    static_assert(SS == lane_stage_stride(NX, NU), "layout");
+    static_assert(NX * NX <= SS, "Riccati scratch W fits one stage");
+};
+
+struct LaneWork {
+    double* ws;  // ceil(B/64) blocks of lane_ws_doubles(nx, nu, N) x 64 doubles
+};
+
+// packed upper-triangle index of (i, j), i <= j, of an n x n symmetric matrix
+__host__ __device__ constexpr int sym_idx(int n, int i, int j) {
+    return i <= j ? i * n - i * (i - 1) / 2 + (j - i) : j * n - j * (j - 1) / 2 + (i - j);
+}
+
+// Products with the discrete stage matrices of a second-order model (x = [q; qd], xdot = [qd; acc]):
+//   A = I + h f_x = [[I, h I], [hFq, I + hFqd]],   B = h f_u = [[0], [hFu]]
+// where hFq = h dacc/dq, hFqd = h dacc/dqd, hFu = h dacc/du (row-major NQ x NQ / NQ x NU).
+template <int NQ>
+MMPC_HD void a_mul(double h, const double* hFq, const double* hFqd, const double* v, double* out) {
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        double t = v[NQ + i];
+#pragma unroll
+        for (int s = 0; s < NQ; ++s) t = fma(hFq[i * NQ + s], v[s], fma(hFqd[i * NQ + s], v[NQ + s], t));
+        out[NQ + i] = t;
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) out[i] = fma(h, v[NQ + i], v[i]);
+}
+template <int NQ>
+MMPC_HD void at_mul(double h, const double* hFq, const double* hFqd, const double* v, double* out) {
+#pragma unroll
+    for (int a = 0; a < NQ; ++a) {
+        double tq = v[a], td = fma(h, v[a], v[NQ + a]);
+#pragma unroll
+        for (int s = 0; s < NQ; ++s) {
+            tq = fma(hFq[s * NQ + a], v[NQ + s], tq);
+            td = fma(hFqd[s * NQ + a], v[NQ + s], td);
+        }
+        out[a] = tq;
+        out[NQ + a] = td;
+    }
+}
+
+// Per-lane pointer to stage k of the workspace, opaque to the optimiser: every access of a stage loop is
+// derived from it (offset folded into the instruction or one add), so nothing is hoisted out of the loop.
+// Without it LICM materialises one 64-bit offset per (field, element) before the loop and spills them.
+__device__ __forceinline__ double* stage_ptr(double* wsb, int64_t k, int SS, int lane) {
+    double* q = wsb + k * SS * 64 + lane;
+    asm volatile("" : "+v"(q));
+    return q;
+}
+
+template <class Model>
+__global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw) {
+    constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NS = NX + NU, ND = NX + NU;
+    static_assert(NX == 2 * NQ, "second-order models only (x = [q; qd])");
+    const int64_t inst = blockIdx.x * (int64_t)64 + threadIdx.x;
+    // Riccati matrix P~ (packed upper, NS(NS+1)/2 doubles per lane) lives in LDS, lane-interleaved
+    // (conflict-free): holding it in registers next to the stage blocks and the factor spills to scratch.
+    __shared__ double sP[NS * (NS + 1) / 2][64];
+    if (inst >= p.B) return;  // lanes never exchange data
+    double* __restrict__ Pl = &sP[0][threadIdx.x];
+#define PS(i, j) Pl[sym_idx(NS, (i), (j)) * 64]
+    const int N = p.N;
+    const int NV = NX * (N + 1) + NU * N;
+    const double h = p.h;
+    using SF = StageFields<NX, NU>;
+    constexpr int SS = SF::SS;
+    const int lane = threadIdx.x;
+    double* __restrict__ const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)(N + 3) * SS * 64);  // wave-uniform
+#define ST(k, f, e) wsb[((int64_t)(k) * SS + (f) + (e)) * 64 + lane]  // one-off accesses
+#define SK(dk, f, e) sk[((dk) * SS + (f) + (e)) * 64]                   // stage k + dk inside a stage loop
+
+    const double* w = p.weights + inst * p.w_stride;
+    double Q[NX], R[NU], Rm[NU], up[NU];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) Q[r] = w[r];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        R[c] = w[NX + c];
+        Rm[c] = w[NX + NU + c];
+        up[c] = p.u_prev[inst * NU + c];
+    }
+    // ---- load: V (reference layout) -> SoA X/U, x_0 pinned (ModelControl.cpp:144-145), targets ----
+    {
+        const double* Vin = p.V + inst * (int64_t)NV;
+        for (int k = 0; k < N; ++k) {
+#pragma unroll
+            for (int r = 0; r < NX; ++r) ST(k, SF::X, r) = (k == 0) ? p.x0[inst * NX + r] : Vin[k * ND + r];
+#pragma unroll
+            for (int c = 0; c < NU; ++c) ST(k, SF::U, c) = Vin[k * ND + NX + c];
+        }
+#pragma unroll
+        for (int r = 0; r < NX; ++r) ST(N, SF::X, r) = Vin[N * ND + r];
+        const double* tr = p.traj + inst * (int64_t)N * NX;
+        for (int k = 0; k < N; ++k)
+#pragma unroll
+            for (int r = 0; r < NX; ++r) ST(k, SF::R, r) = tr[k * NX + r];
+    }
+    // linear mode: acceleration Jacobians and xdot at (state, control) = (x_0, u_prev), ModelControl.cpp:125-135
+    const bool lin = p.is_linear != 0;
+    constexpr int LFQ = 0, LFQD = NQ * NQ, LFU = 2 * NQ * NQ, LXD = 2 * NQ * NQ + NQ * NU, LXS = LXD + NX,
+                  LUS = LXS + NX;
+    static_assert(LUS + NU <= SS, "linear-mode block fits one stage");
+    if (lin) {
+        double x[NX], acc[NQ], Fq[NQ * NQ], Fqd[NQ * NQ], Fu[NQ * NU];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) x[r] = ST(0, SF::X, r);
+        Model::eval_acc_jac(x, up, acc, Fq, Fqd, Fu);
+#pragma unroll
+        for (int t = 0; t < NQ * NQ; ++t) {
+            ST(N + 1, LFQ, t) = Fq[t];
+            ST(N + 1, LFQD, t) = Fqd[t];
+        }
+#pragma unroll
+        for (int t = 0; t < NQ * NU; ++t) ST(N + 1, LFU, t) = Fu[t];
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) {
+            ST(N + 1, LXD, t) = x[NQ + t];
+            ST(N + 1, LXD, NQ + t) = acc[t];
+        }
+#pragma unroll
+        for (int t = 0; t < NX; ++t) ST(N + 1, LXS, t) = x[t];
+#pragma unroll
+        for (int t = 0; t < NU; ++t) ST(N + 1, LUS, t) = up[t];
+    }
+    // Stage model: xd = f(x, u) and (jac) the SCALED blocks hFq, hFqd, hFu of A_k, B_k.
+    // Linear mode: F_lin of ModelGenerator.cpp:47-48 with the stored A*, B*, xdot*.
+#define STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, jac)                                                        \
+    do {                                                                                                 \
+        if (!lin) {                                                                                      \
+            if (jac) {                                                                                   \
+                Model::eval_acc_jac(x, u, xd + NQ, hFq, hFqd, hFu);                                      \
+                _Pragma("unroll") for (int i_ = 0; i_ < NQ; ++i_) xd[i_] = x[NQ + i_];                   \
+            } else {                                                                                     \
+                Model::eval(x, u, xd);                                                                   \
+            }                                                                                            \
+        } else {                                                                                         \
+            double* const lp_ = stage_ptr(wsb, N + 1, SS, lane);                                         \
+            double dx_[NX], du_[NU];                                                                     \
+            _Pragma("unroll") for (int i_ = 0; i_ < NX; ++i_) dx_[i_] = x[i_] - lp_[((LXS) + (i_)) * 64];        \
+            _Pragma("unroll") for (int i_ = 0; i_ < NU; ++i_) du_[i_] = u[i_] - lp_[((LUS) + (i_)) * 64];        \
+            _Pragma("unroll") for (int i_ = 0; i_ < NQ; ++i_) {                                          \
+                xd[i_] = lp_[((LXD) + (i_)) * 64] + dx_[NQ + i_];                                                \
+                double t_ = lp_[((LXD) + (NQ + i_)) * 64];                                                       \
+                _Pragma("unroll") for (int s_ = 0; s_ < NQ; ++s_) {                                      \
+                    const double fq_ = lp_[((LFQ) + (i_ * NQ + s_)) * 64], fd_ = lp_[((LFQD) + (i_ * NQ + s_)) * 64];   \
+                    if (jac) {                                                                           \
+                        hFq[i_ * NQ + s_] = fq_;                                                         \
+                        hFqd[i_ * NQ + s_] = fd_;                                                        \
+                    }                                                                                    \
+                    t_ = fma(fq_, dx_[s_], fma(fd_, dx_[NQ + s_], t_));                                  \
+                }                                                                                        \
+                _Pragma("unroll") for (int c_ = 0; c_ < NU; ++c_) {                                      \
+                    const double fu_ = lp_[((LFU) + (i_ * NU + c_)) * 64];                                       \
+                    if (jac) hFu[i_ * NU + c_] = fu_;                                                    \
+                    t_ = fma(fu_, du_[c_], t_);                                                          \
+                }                                                                                        \
+                xd[NQ + i_] = t_;                                                                        \
+            }                                                                                            \
+        }                                                                                                \
+        if (jac) {                                                                                       \
+            _Pragma("unroll") for (int i_ = 0; i_ < NQ * NQ; ++i_) {                                     \
+                hFq[i_] *= h;                                                                            \
+                hFqd[i_] *= h;                                                                           \
+            }                                                                                            \
+            _Pragma("unroll") for (int i_ = 0; i_ < NQ * NU; ++i_) hFu[i_] *= h;                         \
+        }                                                                                                \
+    } while (0)
+
+    int status = ST_MAX_ITER;
+    int it = 0;
+    double kkt = 0.0, mu = 0.0;
+    #pragma unroll 1
+    for (it = 0; it <= p.max_iter; ++it) {
+        // ---- (1) forward: F, defects, d_{k+1} = A_k d_k + c_k, merit value ----
+        double J0 = 0.0, c1 = 0.0, cmax = 0.0;
+        bool nonfinite = false;
+        {
+            double d[NX], xk[NX], um[NU];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                d[r] = 0.0;
+                xk[r] = ST(0, SF::X, r);
+            }
+#pragma unroll
+            for (int c = 0; c < NU; ++c) um[c] = up[c];
+            #pragma unroll 1
+            for (int k = 0; k < N; ++k) {
+                double* const sk = stage_ptr(wsb, k, SS, lane);
+                double u[NU], xn[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+#pragma unroll
+                for (int c = 0; c < NU; ++c) u[c] = SK(0, SF::U, c);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) xn[r] = SK(1, SF::X, r);
+                STAGE_EVAL(xk, u, xd, hFq, hFqd, hFu, true);
+                double dn[NX];
+                a_mul<NQ>(h, hFq, hFqd, d, dn);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    const double F = fma(h, xd[r], xk[r]);
+                    const double c = F - xn[r];
+                    SK(0, SF::C, r) = c;
+                    cmax = fmax(cmax, fabs(c));
+                    c1 += fabs(c);
+                    nonfinite |= !isfinite(c);
+                    const double e = F - SK(0, SF::R, r);
+                    J0 = fma(e * Q[r], e, J0);
+                    d[r] = dn[r] + c;
+                    SK(1, SF::D, r) = d[r];
+                    xk[r] = xn[r];
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const double dif = u[c] - um[c];
+                    J0 = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], J0));
+                    um[c] = u[c];
+                }
+            }
+        }
+
+        // ---- (2) backward: adjoint + reduced gradient (stopping test) and the Riccati recursion ----
+        // Value function V_k(s) = s^T P s + 2 p^T s on s = [dx_k; du_{k-1}] (no 1/2: J has none,
+        // ModelGenerator.cpp:208-222); (P, pv) hold P~_{k+1} = P_{k+1} + blkdiag(Q, 0) on entry to step k.
+        double gmax = 0.0, lmax = 0.0;
+        bool fact_ok = true;
+        {
+            double pv[NS], lam[NX], unext[NU];
+#pragma unroll
+            for (int a = 0; a < NS; ++a) {
+                pv[a] = 0.0;
+#pragma unroll
+                for (int b = a; b < NS; ++b) PS(a, b) = (a == b && a < NX) ? Q[a] : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                const double eb = ST(N, SF::X, r) - ST(N - 1, SF::R, r);  // x_N - r_{N-1}
+                pv[r] = Q[r] * eb;
+                lam[r] = Q[r] * (ST(N, SF::D, r) + eb);  // lam_N = Q e_{N-1}
+                lmax = fmax(lmax, fabs(lam[r]));
+            }
+#pragma unroll
+            for (int c = 0; c < NU; ++c) unext[c] = 0.0;
+            #pragma unroll 1
+            for (int k = N - 1; k >= 0; --k) {
+                double* const sk = stage_ptr(wsb, k, SS, lane);
+                double x[NX], u[NU], um[NU], cc[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    x[r] = SK(0, SF::X, r);
+                    cc[r] = SK(0, SF::C, r);
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    u[c] = SK(0, SF::U, c);
+                    um[c] = (k == 0) ? up[c] : SK(-1, SF::U, c);
+                }
+                STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                // reduced gradient g_k = B_k^T lam_{k+1} + R/Rm terms (same expression as sqp_wave.h)
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    double g = 0.0;
+#pragma unroll
+                    for (int s = 0; s < NQ; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
+                    g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
+                    if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
+                    gmax = fmax(gmax, fabs(2.0 * g));
+                    nonfinite |= !isfinite(g);
+                    unext[c] = u[c];
+                }
+                // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1},  e_{k-1} = d_k + x_k - r_{k-1}
+                if (k >= 1) {
+                    double ln[NX];
+                    at_mul<NQ>(h, hFq, hFqd, lam, ln);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        lam[r] = fma(Q[r], SK(0, SF::D, r) + x[r] - SK(-1, SF::R, r), ln[r]);
+                        lmax = fmax(lmax, fabs(lam[r]));
+                    }
+                }
+                // ---- Riccati step ----
+                double G[NX][NU];  // P_xx B + P_xu   (B = [0; hFu])
+#pragma unroll
+                for (int r = 0; r < NX; ++r)
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {
+                        double t = PS(r, NX + c);
+#pragma unroll
+                        for (int s = 0; s < NQ; ++s) t = fma(PS(r, NQ + s), hFu[s * NU + c], t);
+                        G[r][c] = t;
+                    }
+                double mv[NX];  // P_xx c + p_x
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    double t = pv[r];
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) t = fma(PS(r, q), cc[q], t);
+                    mv[r] = t;
+                }
+                double Hww[NU][NU], Y[NU][NS + 1];  // Y rows: L^-1 [H_wx | -R | h_w]
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+#pragma unroll
+                    for (int b = a; b < NU; ++b) {
+                        double t = PS(NX + a, NX + b);
+#pragma unroll
+                        for (int s = 0; s < NQ; ++s)
+                            t = fma(hFu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), hFu[s * NU + b], t));
+                        if (a == b) t += R[a] + Rm[a];
+                        Hww[a][b] = t;
+                    }
+                    double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
+#pragma unroll
+                    for (int s = 0; s < NQ; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) t = fma(PS(r, NX + a), cc[r], t);
+                    Y[a][NS] = t;
+                    double ga[NX];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) ga[r] = G[r][a];
+                    at_mul<NQ>(h, hFq, hFqd, ga, &Y[a][0]);  // H_wx row a = (A^T G[:, a])^T
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) Y[a][NX + c] = (a == c) ? -R[a] : 0.0;
+                }
+                // W = P_xx A (row r of W = (A^T P_xx[r][:])^T), streamed through the lane's scratch stage of the
+                // workspace: held in registers next to G, Y and the stage blocks it spills (1.2 KB/lane).
+                // p~_k x part: A^T mv + Q (x_k - r_{k-1}).
+                double pn[NS];
+                double* const sw = stage_ptr(wsb, N + 2, SS, lane);  // per-lane scratch stage
+                if (k >= 1) {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        double prow[NX], wrow[NX];
+#pragma unroll
+                        for (int q = 0; q < NX; ++q) prow[q] = PS(r, q);
+                        at_mul<NQ>(h, hFq, hFqd, prow, wrow);
+#pragma unroll
+                        for (int b = 0; b < NX; ++b) sw[(r * NX + b) * 64] = wrow[b];
+                    }
+                    double t[NX];
+                    at_mul<NQ>(h, hFq, hFqd, mv, t);
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - SK(-1, SF::R, q), t[q]);
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
+                }
+                // Cholesky H_ww = L L^T, then Y <- L^-1 Y
+                double Ld[NU][NU], il[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double s = Hww[a][a];
+#pragma unroll
+                    for (int q = 0; q < a; ++q) s = fma(-Ld[a][q], Ld[a][q], s);
+                    fact_ok &= (s > 0.0) && isfinite(s);
+                    const double lj = sqrt(fmax(s, 1e-300));
+                    Ld[a][a] = lj;
+                    il[a] = 1.0 / lj;
+#pragma unroll
+                    for (int b = a + 1; b < NU; ++b) {
+                        double t = Hww[a][b];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
+                        Ld[b][a] = t * il[a];
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int j = 0; j <= NS; ++j) {
+                        double t = Y[a][j];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
+                        Y[a][j] = t * il[a];
+                    }
+                // [K_k | kff_k] = -L^-T Y
+                {
+                    double Kt[NU][NS + 1];
+#pragma unroll
+                    for (int a = NU - 1; a >= 0; --a)
+#pragma unroll
+                        for (int j = 0; j <= NS; ++j) {
+                            double t = Y[a][j];
+#pragma unroll
+                            for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], Kt[q][j], t);
+                            Kt[a][j] = t * il[a];
+                        }
+#pragma unroll
+                    for (int a = 0; a < NU; ++a)
+#pragma unroll
+                        for (int j = 0; j <= NS; ++j) SK(0, SF::K, a * (NS + 1) + j) = -Kt[a][j];
+                }
+                if (k == 0) break;  // s_0 = 0: P~_0 is never used
+                // P~_k = blkdiag(A^T W + Q, R) - Y^T Y (old P is dead: overwrite it in place), p~_k = pn - Y^T y
+                asm volatile("" ::: "memory");  // W comes back from memory, not from forwarded registers
+#pragma unroll
+                for (int b = 0; b < NX; ++b) {
+                    double wcol[NX], col[NX];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) wcol[r] = sw[(r * NX + b) * 64];
+                    at_mul<NQ>(h, hFq, hFqd, wcol, col);
+#pragma unroll
+                    for (int a = 0; a <= b; ++a) {
+                        double v = col[a] + ((a == b) ? Q[a] : 0.0);
+#pragma unroll
+                        for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
+                        PS(a, b) = v;
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < NS; ++a) {
+                    double t = pn[a];
+#pragma unroll
+                    for (int q = 0; q < NU; ++q) t = fma(-Y[q][a], Y[q][NS], t);
+                    pv[a] = t;
+#pragma unroll
+                    for (int b = (a < NX ? NX : a); b < NS; ++b) {
+                        double v = (a == b) ? R[a - NX] : 0.0;
+#pragma unroll
+                        for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
+                        PS(a, b) = v;
+                    }
+                }
+            }
+        }
+        kkt = fmax(gmax, cmax);
+        // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
+        double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
+        if (trc) {
+            trc[0] = gmax;
+            trc[1] = cmax;
+            trc[2] = J0;
+            trc[3] = c1;
+            trc[7] = lmax;
+        }
+        if (nonfinite || !isfinite(kkt)) {
+            status = ST_NONFINITE;
+            break;
+        }
+        if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
+            status = ST_CONVERGED;
+            break;
+        }
+        if (it == p.max_iter) {
+            status = ST_MAX_ITER;
+            break;
+        }
+        if (!fact_ok) {
+            status = ST_FACT_FAILED;
+            break;
+        }
+
+        // ---- (3) forward: step (dx, du) and the directional derivative of J ----
+        double dJ = 0.0;
+        {
+            double dx[NX], dup[NU], um[NU];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                dx[r] = 0.0;
+                ST(0, SF::DX, r) = 0.0;
+            }
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                dup[c] = 0.0;
+                um[c] = up[c];
+            }
+            #pragma unroll 1
+            for (int k = 0; k < N; ++k) {
+                double* const sk = stage_ptr(wsb, k, SS, lane);
+                double x[NX], u[NU], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) x[r] = SK(0, SF::X, r);
+#pragma unroll
+                for (int c = 0; c < NU; ++c) u[c] = SK(0, SF::U, c);
+                STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                double du[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    const int base = a * (NS + 1);
+                    double t = SK(0, SF::K, base + NS);
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) t = fma(SK(0, SF::K, base + q), dx[q], t);
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) t = fma(SK(0, SF::K, base + NX + c), dup[c], t);
+                    du[a] = t;
+                    SK(0, SF::DU, a) = t;
+                }
+                double ad[NX];
+                a_mul<NQ>(h, hFq, hFqd, dx, ad);
+#pragma unroll
+                for (int s = 0; s < NQ; ++s)
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    const double F = fma(h, xd[r], x[r]);
+                    const double qe = 2.0 * Q[r] * (F - SK(0, SF::R, r));
+                    dJ = fma(qe, ad[r], dJ);
+                    dx[r] = ad[r] + SK(0, SF::C, r);
+                    SK(1, SF::DX, r) = dx[r];
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const double dif = u[c] - um[c];
+                    dJ = fma(2.0 * R[c] * dif, du[c] - dup[c], fma(2.0 * Rm[c] * u[c], du[c], dJ));
+                    um[c] = u[c];
+                    dup[c] = du[c];
+                }
+            }
+        }
+
+        // ---- (4) l1-merit Armijo line search (noise-aware, as sqp_wave.h) ----
+        mu = fmax(mu, 4.0 * lmax + 1.0);
+        const double phi0 = fma(mu, c1, J0);
+        const double dphi = dJ - mu * c1;
+        double alpha = 1.0;
+        bool accepted = false;
+        #pragma unroll 1
+        for (int ls = 0; ls < 30; ++ls) {
+            double Jt = 0.0, ct = 0.0, xk[NX], umt[NU];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) xk[r] = ST(0, SF::X, r);  // dx_0 = 0
+#pragma unroll
+            for (int c = 0; c < NU; ++c) umt[c] = up[c];
+            #pragma unroll 1
+            for (int k = 0; k < N; ++k) {
+                double* const sk = stage_ptr(wsb, k, SS, lane);
+                double u[NU], xn[NX], xd[NX];
+#pragma unroll
+                for (int c = 0; c < NU; ++c) u[c] = fma(alpha, SK(0, SF::DU, c), SK(0, SF::U, c));
+#pragma unroll
+                for (int r = 0; r < NX; ++r) xn[r] = fma(alpha, SK(1, SF::DX, r), SK(1, SF::X, r));
+                {
+                    double* nil_ = nullptr;
+                    STAGE_EVAL(xk, u, xd, nil_, nil_, nil_, false);
+                }
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    const double F = fma(h, xd[r], xk[r]);
+                    const double er = F - SK(0, SF::R, r);
+                    Jt = fma(er * Q[r], er, Jt);
+                    ct += fabs(F - xn[r]);
+                    xk[r] = xn[r];
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const double dif = u[c] - umt[c];
+                    Jt = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], Jt));
+                    umt[c] = u[c];
+                }
+            }
+            const double phit = fma(mu, ct, Jt);
+            const double noise = 1.0 + fabs(phi0);
+            if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) {
+                accepted = true;
+                break;
+            }
+            alpha *= 0.5;
+        }
+        if (trc) {
+            trc[4] = dJ;
+            trc[5] = alpha;
+            trc[6] = mu;
+        }
+        if (!accepted) {
+            status = ST_LS_FAILED;
+            break;
+        }
+        #pragma unroll 1
+        for (int k = 0; k <= N; ++k) {
+                double* const sk = stage_ptr(wsb, k, SS, lane);
+            if (k > 0) {
+#pragma unroll
+                for (int r = 0; r < NX; ++r) SK(0, SF::X, r) = fma(alpha, SK(0, SF::DX, r), SK(0, SF::X, r));
+            }
+            if (k < N) {
+#pragma unroll
+                for (int c = 0; c < NU; ++c) SK(0, SF::U, c) = fma(alpha, SK(0, SF::DU, c), SK(0, SF::U, c));
+            }
+        }
+    }
+
+    // ---- bounds check (box constraints are reported, not yet enforced), as sqp_wave.h ----
+    if (status == ST_CONVERGED && (p.u_lb || p.u_ub)) {
+        bool viol = false;
+        for (int k = 0; k < N; ++k)
+#pragma unroll
+            for (int r = 0; r < NU; ++r) {
+                const double u = ST(k, SF::U, r);
+                if (p.u_lb) viol |= (p.u_lb[r] > -1e19) && (u < p.u_lb[r] - 1e-9);
+                if (p.u_ub) viol |= (p.u_ub[r] < 1e19) && (u > p.u_ub[r] + 1e-9);
+            }
+        if (viol) status = ST_BOUNDS;
+    }
+    // ---- write back V (reference layout) ----
+    double* Vout = p.V + inst * (int64_t)NV;
+    for (int k = 0; k < N; ++k) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) Vout[k * ND + r] = ST(k, SF::X, r);
+#pragma unroll
+        for (int c = 0; c < NU; ++c) Vout[k * ND + NX + c] = ST(k, SF::U, c);
+    }
+#pragma unroll
+    for (int r = 0; r < NX; ++r) Vout[N * ND + r] = ST(N, SF::X, r);
+    if (p.status) p.status[inst] = status;
+    if (p.iters) p.iters[inst] = it;
+    if (p.kkt) p.kkt[inst] = kkt;
+#undef ST
+#undef SK
+#undef PS
+#undef STAGE_EVAL
+}
+
+}  // namespace mmpc

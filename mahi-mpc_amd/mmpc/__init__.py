@@ -39,9 +39,13 @@ class MmpcError(RuntimeError):
         self.code = code
 
 
+KKT_AUTO, KKT_CONDENSED, KKT_RICCATI = 0, 1, 2
+MODEL_TWO_LINK_ARM, MODEL_EXO_ARM = 0, 1
+
+
 class Opts(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("device", C.c_int32), ("tol_grad", C.c_double),
-                ("tol_defect", C.c_double)]
+                ("tol_defect", C.c_double), ("kkt_solver", C.c_int32), ("reserved", C.c_int32)]
 
 
 class ModelInfo(C.Structure):
@@ -84,6 +88,7 @@ def lib():
         L.mmpc_destroy.argtypes = [_vp]
         L.mmpc_get_model_info.argtypes = [_vp, C.POINTER(ModelInfo)]
         L.mmpc_set_opts.argtypes = [_vp, C.POINTER(Opts)]
+        L.mmpc_reserve_workspace.argtypes = [_vp, C.c_int64, C.POINTER(C.c_uint64)]
         L.mmpc_solve_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 7
         L.mmpc_solve_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 6
         L.mmpc_linearize_batch.argtypes = [_vp, C.c_int64] + [_vp] * 6
@@ -109,9 +114,10 @@ def default_opts() -> Opts:
 
 
 def write_model_json(path, name, num_x, num_u, step_size_us, num_shooting_nodes, is_linear=False,
-                     u_min=None, u_max=None, x_min=None, x_max=None, dll_filepath="", extra=None):
+                     u_min=None, u_max=None, x_min=None, x_max=None, dll_filepath="", extra=None, model=None):
     """Write <name>.json exactly as ModelGenerator::save_param_file does (ModelParameters.cpp:37-50),
-    including the +-10e30 defaults of the ModelParameters constructor (ModelParameters.cpp:14-24)."""
+    including the +-10e30 defaults of the ModelParameters constructor (ModelParameters.cpp:14-24).
+    ``model`` ("two_link_arm" / "exo_arm") adds the "mmpc_model" key naming the built-in dynamics."""
     def dflt(v, n, s):
         return list(v) if v is not None else [s * 10e30] * n
     m = {"name": name, "timespan": int(step_size_us) * int(num_shooting_nodes), "step_size": int(step_size_us),
@@ -119,6 +125,8 @@ def write_model_json(path, name, num_x, num_u, step_size_us, num_shooting_nodes,
          "x_min": dflt(x_min, num_x, -1), "u_min": dflt(u_min, num_u, -1),
          "x_max": dflt(x_max, num_x, 1), "u_max": dflt(u_max, num_u, 1),
          "dll_filepath": dll_filepath, "is_linear": bool(is_linear)}
+    if model:
+        m["mmpc_model"] = model
     if extra:
         m.update(extra)
     with open(path, "w") as fh:
@@ -151,8 +159,10 @@ class Solver:
     """One loaded model (the reference's ModelControl without the thread/bookkeeping)."""
 
     def __init__(self, model_json=None, json_text=None, max_iter=None, tol_grad=None, tol_defect=None,
-                 device=None):
+                 device=None, kkt_solver=None):
         o = default_opts()
+        if kkt_solver is not None:
+            o.kkt_solver = kkt_solver
         if max_iter is not None:
             o.max_iter = max_iter
         if tol_grad is not None:
@@ -173,6 +183,12 @@ class Solver:
         self.nx, self.nu, self.N = info.num_x, info.num_u, info.num_shooting_nodes
         self.NV = info.num_v
         self.h = info.step_size
+
+    def reserve_workspace(self, B) -> int:
+        """Pre-allocate the Riccati solver workspace for up to B instances; returns its size in bytes."""
+        n = C.c_uint64(0)
+        _check(lib().mmpc_reserve_workspace(self._h, B, C.byref(n)))
+        return int(n.value)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -248,6 +264,33 @@ def flops_per_iteration(N: int, nx: int = 4, nu: int = 2) -> dict:
     f["gauss_jordan"] = sum(2 * (M - 1) * (M - k) for k in range(M)) + M  # rows x remaining cols, + rhs
     f["dx_recursion"] = N * (2 * nx * nx + 2 * nu * nx + nx)
     f["merit"] = N * (2 * nx * (nx + nu) + 12)
+    f["total"] = sum(f.values())
+    return f
+
+
+def riccati_flops_per_iteration(N: int, nx: int = 8, nu: int = 4) -> dict:
+    """Algorithmic flop count (mul+add = 2) of ONE SQP iteration of the lane-per-instance Riccati kernel
+    (sqp_lane.h), structure-exploiting for second-order models (A = [[I, hI],[hFq, I+hFqd]],
+    B = [[0],[hFu]], nq = nx/2).  Model evaluations are excluded (SURVEY.md 8d counts them separately)."""
+    nq, ns = nx // 2, nx + nu
+    at_mul = 2 * nq * nx + 2 * nx            # A^T v or A v with the block structure
+    f = {}
+    f["defect_recursion"] = N * (at_mul + nx)
+    f["adjoint_gradient"] = N * (at_mul + 2 * nq * nu + 6 * nu)
+    st = 0
+    st += nx * nu * 2 * nq                    # G = P_xx B + P_xu
+    st += 2 * nx * nx                         # mv = P_xx c + p_x
+    st += nu * (nu + 1) // 2 * 4 * nq         # H_ww
+    st += nu * (2 * nq + 2 * nx + 4)          # h_w
+    st += nu * at_mul                         # H_wx = (A^T G)^T
+    st += nx * (nx * (2 * nq + 2) + at_mul)   # A^T P_xx A by columns
+    st += at_mul + 2 * nx                     # p_x
+    st += nu ** 3 // 3 + nu * nu * (ns + 1)   # Cholesky + forward solve
+    st += nu * nu * (ns + 1)                  # back solve (K)
+    st += ns * (ns + 1) // 2 * 2 * nu + ns * 2 * nu  # P~ = ... - Y^T Y, p~
+    f["riccati"] = N * st
+    f["step_recursion"] = N * (2 * nu * ns + at_mul + 2 * nq * nu + nx)
+    f["merit"] = N * (4 * nx + 8 * nu)
     f["total"] = sum(f.values())
     return f
 

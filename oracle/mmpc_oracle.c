@@ -5,6 +5,8 @@
  *
  * What is restated, and from where (paths relative to the reference root):
  *   dynamics      examples/ex_model_generate.cpp:24-43 (2-link arm, L=m=1, g=9.81)
+ *                 src/inverseTest.cpp:59-74 (exo M(q), via exo_model_gen.h, with the build-defined
+ *                 parameters / gravity / damping of tests/golden/exo_params.json -- not reference-pinned)
  *   Euler step    src/Mahi/Mpc/ModelGenerator.cpp:33-34     F(x,u) = x + h f(x,u)
  *   F_lin         src/Mahi/Mpc/ModelGenerator.cpp:45-48
  *   V layout      src/Mahi/Mpc/ModelGenerator.cpp:61-112    [x0,u0,x1,u1,...,x_{N-1},u_{N-1},xN]
@@ -25,26 +27,36 @@
 #include <omp.h>
 #endif
 
-#define NX 4
-#define NU 2
-#define ND (NX + NU)
+#include "exo_model_gen.h"
 
-/* ---------------- forward-mode dual numbers (6 tangents: x then u) ---------------- */
-typedef struct { double v; double d[ND]; } dual;
+/* model context of the calling thread: dimensions and dynamics (set by set_model) */
+static _Thread_local int t_model = ORACLE_MODEL_TWO_LINK_ARM, t_nx = 4, t_nu = 2;
+#define NX t_nx
+#define NU t_nu
+#define ND (t_nx + t_nu)
+static int set_model(int model) {
+    if (model == ORACLE_MODEL_TWO_LINK_ARM) { t_model = model; t_nx = 4; t_nu = 2; return 0; }
+    if (model == ORACLE_MODEL_EXO_ARM) { t_model = model; t_nx = 8; t_nu = 4; return 0; }
+    return -1;
+}
+
+/* ---------------- forward-mode dual numbers (6 tangents: x then u of the 2-link arm) ---------------- */
+#define DK 6
+typedef struct { double v; double d[DK]; } dual;
 
 static dual dc(double c) { dual r; r.v = c; memset(r.d, 0, sizeof r.d); return r; }
 static dual dvar(double v, int i) { dual r = dc(v); r.d[i] = 1.0; return r; }
-static dual dadd(dual a, dual b) { dual r; r.v = a.v + b.v; for (int i = 0; i < ND; ++i) r.d[i] = a.d[i] + b.d[i]; return r; }
-static dual dsub(dual a, dual b) { dual r; r.v = a.v - b.v; for (int i = 0; i < ND; ++i) r.d[i] = a.d[i] - b.d[i]; return r; }
-static dual dmul(dual a, dual b) { dual r; r.v = a.v * b.v; for (int i = 0; i < ND; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i]; return r; }
-static dual dscale(double s, dual a) { dual r; r.v = s * a.v; for (int i = 0; i < ND; ++i) r.d[i] = s * a.d[i]; return r; }
+static dual dadd(dual a, dual b) { dual r; r.v = a.v + b.v; for (int i = 0; i < DK; ++i) r.d[i] = a.d[i] + b.d[i]; return r; }
+static dual dsub(dual a, dual b) { dual r; r.v = a.v - b.v; for (int i = 0; i < DK; ++i) r.d[i] = a.d[i] - b.d[i]; return r; }
+static dual dmul(dual a, dual b) { dual r; r.v = a.v * b.v; for (int i = 0; i < DK; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i]; return r; }
+static dual dscale(double s, dual a) { dual r; r.v = s * a.v; for (int i = 0; i < DK; ++i) r.d[i] = s * a.d[i]; return r; }
 static dual ddiv(dual a, dual b) {
     dual r; r.v = a.v / b.v;
-    for (int i = 0; i < ND; ++i) r.d[i] = (a.d[i] - r.v * b.d[i]) / b.v;
+    for (int i = 0; i < DK; ++i) r.d[i] = (a.d[i] - r.v * b.d[i]) / b.v;
     return r;
 }
-static dual dsin(dual a) { dual r; r.v = sin(a.v); double c = cos(a.v); for (int i = 0; i < ND; ++i) r.d[i] = c * a.d[i]; return r; }
-static dual dcos(dual a) { dual r; r.v = cos(a.v); double s = -sin(a.v); for (int i = 0; i < ND; ++i) r.d[i] = s * a.d[i]; return r; }
+static dual dsin(dual a) { dual r; r.v = sin(a.v); double c = cos(a.v); for (int i = 0; i < DK; ++i) r.d[i] = c * a.d[i]; return r; }
+static dual dcos(dual a) { dual r; r.v = cos(a.v); double s = -sin(a.v); for (int i = 0; i < DK; ++i) r.d[i] = s * a.d[i]; return r; }
 static dual dneg(dual a) { return dscale(-1.0, a); }
 
 /* 2-link arm ODE right-hand side, restated from examples/ex_model_generate.cpp:36-37
@@ -86,15 +98,83 @@ static void two_link_dual(const dual* x, const dual* u, dual* xd) {
 }
 
 void oracle_two_link_jac(const double* x, const double* u, double* A, double* B, double* xdot) {
-    dual xv[NX], uv[NU], xd[NX];
-    for (int i = 0; i < NX; ++i) xv[i] = dvar(x[i], i);
-    for (int i = 0; i < NU; ++i) uv[i] = dvar(u[i], NX + i);
+    dual xv[4], uv[2], xd[4];
+    for (int i = 0; i < 4; ++i) xv[i] = dvar(x[i], i);
+    for (int i = 0; i < 2; ++i) uv[i] = dvar(u[i], 4 + i);
     two_link_dual(xv, uv, xd);
-    for (int r = 0; r < NX; ++r) {
+    for (int r = 0; r < 4; ++r) {
         if (xdot) xdot[r] = xd[r].v;
-        if (A) for (int c = 0; c < NX; ++c) A[r * NX + c] = xd[r].d[c];
-        if (B) for (int c = 0; c < NU; ++c) B[r * NU + c] = xd[r].d[NX + c];
+        if (A) for (int c = 0; c < 4; ++c) A[r * 4 + c] = xd[r].d[c];
+        if (B) for (int c = 0; c < 2; ++c) B[r * 2 + c] = xd[r].d[4 + c];
     }
+}
+
+/* ---------------- 4-DoF exo ----------------
+ * xdot = [qd; M(q)^-1 (tau - D qd - G(q))], G_i = g_i sin q_i.  Dense Gauss-Jordan inverse of M (a different
+ * factorisation from the device's Cholesky) and the symbolic dM/dq_j of exo_model_gen.h:
+ *   d qdd/dq_j = M^-1 (-dM/dq_j qdd - g_j cos q_j e_j),  d qdd/dqd = -M^-1 D,  d qdd/dtau = M^-1. */
+static void inv4(const double* M, double* Minv) {
+    double a[4][8];
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 8; ++c) a[r][c] = (c < 4) ? M[r * 4 + c] : (c - 4 == r ? 1.0 : 0.0);
+    for (int k = 0; k < 4; ++k) {
+        int piv = k;
+        for (int r = k + 1; r < 4; ++r) if (fabs(a[r][k]) > fabs(a[piv][k])) piv = r;
+        for (int c = 0; c < 8; ++c) { double t = a[k][c]; a[k][c] = a[piv][c]; a[piv][c] = t; }
+        double f = 1.0 / a[k][k];
+        for (int c = 0; c < 8; ++c) a[k][c] *= f;
+        for (int r = 0; r < 4; ++r) {
+            if (r == k) continue;
+            double m = a[r][k];
+            for (int c = 0; c < 8; ++c) a[r][c] -= m * a[k][c];
+        }
+    }
+    for (int r = 0; r < 4; ++r) for (int c = 0; c < 4; ++c) Minv[r * 4 + c] = a[r][4 + c];
+}
+
+void oracle_exo_jac(const double* x, const double* u, double* A, double* B, double* xdot) {
+    double M[16], dM[4][16], Minv[16], w[4], qdd[4];
+    exo_mass_and_grad(x, M, dM);
+    inv4(M, Minv);
+    for (int i = 0; i < 4; ++i) w[i] = u[i] - EXO_DAMPING[i] * x[4 + i] - EXO_GRAVITY_GAIN[i] * sin(x[i]);
+    for (int r = 0; r < 4; ++r) {
+        qdd[r] = 0.0;
+        for (int c = 0; c < 4; ++c) qdd[r] += Minv[r * 4 + c] * w[c];
+    }
+    if (xdot) for (int r = 0; r < 4; ++r) { xdot[r] = x[4 + r]; xdot[4 + r] = qdd[r]; }
+    if (A) {
+        for (int i = 0; i < 64; ++i) A[i] = 0.0;
+        for (int r = 0; r < 4; ++r) A[r * 8 + 4 + r] = 1.0;
+        for (int j = 0; j < 4; ++j) {
+            double rhs[4];
+            for (int r = 0; r < 4; ++r) {
+                double t = 0.0;
+                for (int c = 0; c < 4; ++c) t += dM[j][r * 4 + c] * qdd[c];
+                rhs[r] = -t;
+            }
+            rhs[j] -= EXO_GRAVITY_GAIN[j] * cos(x[j]);
+            for (int r = 0; r < 4; ++r) {
+                double t = 0.0;
+                for (int c = 0; c < 4; ++c) t += Minv[r * 4 + c] * rhs[c];
+                A[(4 + r) * 8 + j] = t;
+                A[(4 + r) * 8 + 4 + j] = -Minv[r * 4 + j] * EXO_DAMPING[j];
+            }
+        }
+    }
+    if (B) {
+        for (int i = 0; i < 32; ++i) B[i] = 0.0;
+        for (int r = 0; r < 4; ++r) for (int c = 0; c < 4; ++c) B[(4 + r) * 4 + c] = Minv[r * 4 + c];
+    }
+}
+
+void oracle_exo_mass(const double* q, double* M) {
+    double dM[4][16];
+    exo_mass_and_grad(q, M, dM);
+}
+
+static void model_jac(const double* x, const double* u, double* A, double* B, double* xdot) {
+    if (t_model == ORACLE_MODEL_EXO_ARM) oracle_exo_jac(x, u, A, B, xdot);
+    else oracle_two_link_jac(x, u, A, B, xdot);
 }
 
 void oracle_two_link_xdot(const double* x, const double* u, double* xdot) {
@@ -120,7 +200,7 @@ static _Thread_local const double* g_lin = NULL;
 
 static void stage_jac(const double* x, const double* u, double* A, double* Bc, double* xd) {
     if (!g_lin) {
-        oracle_two_link_jac(x, u, A, Bc, xd);
+        model_jac(x, u, A, Bc, xd);
         return;
     }
     const double *As = g_lin, *Bs = g_lin + NX * NX, *fs = Bs + NX * NU, *xs = fs + NX, *us = xs + NX;
@@ -133,7 +213,7 @@ static void stage_jac(const double* x, const double* u, double* A, double* Bc, d
 }
 
 static void euler_step(double h, const double* x, const double* u, double* F, double* Ad, double* Bd) {
-    double A[NX * NX], Bc[NX * NU], xd[NX];
+    double A[64], Bc[32], xd[8];
     stage_jac(x, u, A, Bc, xd);
     for (int r = 0; r < NX; ++r) {
         F[r] = x[r] + h * xd[r];
@@ -145,7 +225,8 @@ static void euler_step(double h, const double* x, const double* u, double* F, do
 /* J and defects of ModelGenerator.cpp:191-222 at the packed V */
 void oracle_nlp_eval(int model, int N, double h, const double* V, const double* u_prev,
                      const double* traj, const double* w, double* Jout, double* g) {
-    (void)model;  /* nonlinear model; in linear mode solve_one evaluates with g_lin set */
+    /* nonlinear model; in linear mode solve_one evaluates with g_lin set (same thread, same model) */
+    if (!g_lin && set_model(model) != 0) return;
     const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
     double J = 0.0;
     for (int k = 0; k < N; ++k) {
@@ -153,7 +234,7 @@ void oracle_nlp_eval(int model, int N, double h, const double* V, const double* 
         const double* uk = xk + NX;
         const double* xk1 = V + (k + 1) * ND;
         const double* ukm = (k == 0) ? u_prev : V + (k - 1) * ND + NX;
-        double F[NX];
+        double F[8];
         euler_step(h, xk, uk, F, NULL, NULL);
         for (int r = 0; r < NX; ++r) {
             if (g) g[k * NX + r] = F[r] - xk1[r];
@@ -171,7 +252,7 @@ void oracle_nlp_eval(int model, int N, double h, const double* V, const double* 
 void oracle_reduced_gradient(int model, int N, double h, const double* x0, const double* U,
                              const double* u_prev, const double* traj, const double* w,
                              double* grad) {
-    (void)model;
+    if (set_model(model) != 0) return;
     const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
     double* X = (double*)malloc(sizeof(double) * (N + 1) * NX);
     double* Ad = (double*)malloc(sizeof(double) * N * NX * NX);
@@ -179,7 +260,7 @@ void oracle_reduced_gradient(int model, int N, double h, const double* x0, const
     memcpy(X, x0, sizeof(double) * NX);
     for (int k = 0; k < N; ++k) euler_step(h, X + k * NX, U + k * NU, X + (k + 1) * NX, Ad + k * NX * NX, Bd + k * NX * NU);
     /* adjoint: lam_{k} = 2Q(x_{k} - r_{k-1}) + A_k^T lam_{k+1}, lam_N = 2Q(x_N - r_{N-1}) */
-    double lam[NX], tmp[NX];
+    double lam[8], tmp[8];
     for (int r = 0; r < NX; ++r) lam[r] = 2.0 * Q[r] * (X[N * NX + r] - traj[(N - 1) * NX + r]);
     for (int k = N - 1; k >= 0; --k) {
         /* grad wrt u_k: B_k^T lam_{k+1} */
@@ -197,7 +278,7 @@ void oracle_reduced_gradient(int model, int N, double h, const double* x0, const
             for (int r = 0; r < NX; ++r) s += Ad[k * NX * NX + r * NX + c] * lam[r];
             tmp[c] = s + 2.0 * Q[c] * (X[k * NX + c] - traj[(k - 1) * NX + c]);
         }
-        memcpy(lam, tmp, sizeof lam);
+        memcpy(lam, tmp, sizeof(double) * NX);
     }
     free(X); free(Ad); free(Bd);
 }
@@ -320,7 +401,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         /* (3) dense Gamma: rows = x_{k+1} (k<N), cols = u_j (j<=k) */
         memset(s->G, 0, sizeof(double) * (size_t)N * NX * M);
         for (int j = 0; j < N; ++j) {
-            double col[NX][NU], nxt[NX][NU];
+            double col[8][4], nxt[8][4];
             for (int r = 0; r < NX; ++r) for (int q = 0; q < NU; ++q) col[r][q] = s->Bd[j * NX * NU + r * NU + q];
             for (int k = j; k < N; ++k) {
                 if (k > j) {
@@ -398,7 +479,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         if (mu_new > mu) mu = mu_new;
         double J0 = 0.0, c1 = 0.0, dJ = 0.0;
         for (int k = 0; k < N; ++k) {
-            double qe[NX];
+            double qe[8];
             for (int r = 0; r < NX; ++r) {
                 qe[r] = 2.0 * Q[r] * (s->F[k * NX + r] - traj[k * NX + r]);
                 J0 += 0.5 * qe[r] * (s->F[k * NX + r] - traj[k * NX + r]);
@@ -454,7 +535,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
     }
     if (J_out) {
         double J;
-        oracle_nlp_eval(0, N, h, V, u_prev, traj, w, &J, NULL);
+        oracle_nlp_eval(t_model, N, h, V, u_prev, traj, w, &J, NULL);
         *J_out = J;
     }
     *iters_out = it;
@@ -467,7 +548,7 @@ int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, con
                        int64_t w_stride, const double* u_lb, const double* u_ub, int max_iter,
                        double tol_grad, double tol_defect, double* V, int32_t* status,
                        int32_t* iters, double* kkt, double* Jout, int nthreads) {
-    if (model != ORACLE_MODEL_TWO_LINK_ARM || N < 1 || B < 0) return -1;
+    if (set_model(model) != 0 || N < 1 || B < 0) return -1;
     const int NV = NX * (N + 1) + NU * N;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -476,16 +557,17 @@ int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, con
 #endif
 #pragma omp parallel
     {
+        set_model(model);
         ws_t s;
         ws_alloc(&s, N);
 #pragma omp for schedule(dynamic, 4)
         for (int64_t b = 0; b < B; ++b) {
             int32_t it;
             double kk, J;
-            double lin[NX * NX + NX * NU + 3 * NX];
+            double lin[64 + 32 + 3 * 8];
             if (is_linear) {
                 /* A*, B*, xdot* at (state, control) = (x0, u_prev), ModelControl.cpp:125-136 */
-                oracle_two_link_jac(x0 + b * NX, u_prev + b * NU, lin, lin + NX * NX, lin + NX * NX + NX * NU);
+                model_jac(x0 + b * NX, u_prev + b * NU, lin, lin + NX * NX, lin + NX * NX + NX * NU);
                 memcpy(lin + NX * NX + NX * NU + NX, x0 + b * NX, sizeof(double) * NX);
                 memcpy(lin + NX * NX + NX * NU + 2 * NX, u_prev + b * NU, sizeof(double) * NU);
                 g_lin = lin;
@@ -544,6 +626,40 @@ void oracle_synth_two_link(uint64_t seed, int64_t first, int64_t B, int N, doubl
             double sv = a * sin(arg), cv = 2.0 * PI * f * a * cos(arg);
             double* r = traj + (b * N + k) * 4;
             r[0] = sv; r[1] = -sv; r[2] = cv; r[3] = -cv;
+        }
+    }
+}
+
+/* cfg#3 instances: q, qd ~ U[-0.5, 0.5], tau_prev ~ U[-1, 1], per joint a ~ U[0.1, 0.4],
+ * f ~ U[0.25, 1] Hz, phase ~ U[0, 2 pi]; r_k = [a sin(2 pi f t_k + phase); 2 pi f a cos(.)], t_k = k h.
+ * Same recipe as the device generator (mmpc.hip synth_exo_kernel). */
+static double unit_draw_exo(uint64_t seed, int64_t index, int j) {
+    uint64_t v = splitmix64((seed + 0x3C6EF372FE94F82Aull) ^ splitmix64((uint64_t)index * 32ull + (uint64_t)j));
+    return (double)(v >> 11) * 0x1.0p-53;
+}
+
+__attribute__((optimize("-ffp-contract=off")))
+void oracle_synth_exo(uint64_t seed, int64_t first, int64_t B, int N, double h, double* x0, double* u_prev,
+                      double* traj) {
+    const double PI = 3.14159265358979323846;
+    for (int64_t b = 0; b < B; ++b) {
+        int64_t gi = first + b;
+        double a[4], f[4], ph[4];
+        for (int j = 0; j < 4; ++j) {
+            x0[b * 8 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, j));
+            x0[b * 8 + 4 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, 4 + j));
+            u_prev[b * 4 + j] = affine_draw(-1.0, 2.0, unit_draw_exo(seed, gi, 8 + j));
+            a[j] = affine_draw(0.1, 0.3, unit_draw_exo(seed, gi, 12 + j));
+            f[j] = affine_draw(0.25, 0.75, unit_draw_exo(seed, gi, 16 + j));
+            ph[j] = affine_draw(0.0, 2.0 * PI, unit_draw_exo(seed, gi, 20 + j));
+        }
+        for (int k = 0; k < N; ++k) {
+            double* r = traj + (b * N + k) * 8;
+            for (int j = 0; j < 4; ++j) {
+                double arg = 2.0 * PI * f[j] * (k * h) + ph[j];
+                r[j] = a[j] * sin(arg);
+                r[4 + j] = 2.0 * PI * f[j] * a[j] * cos(arg);
+            }
         }
     }
 }

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-enum { ORACLE_MODEL_TWO_LINK_ARM = 0 };
+enum { ORACLE_MODEL_TWO_LINK_ARM = 0, ORACLE_MODEL_EXO_ARM = 1 };
 
 /* per-instance status, same numbering as include/mmpc.h */
 enum {
@@ -38,6 +38,10 @@ enum {
 void oracle_two_link_xdot(const double* x, const double* u, double* xdot);
 /* continuous Jacobians A = df/dx (4x4), B = df/du (4x2), ROW-major, plus xdot */
 void oracle_two_link_jac(const double* x, const double* u, double* A, double* B, double* xdot);
+/* 4-DoF exo (build-defined parameters, tests/golden/exo_params.json):
+ * A = df/dx (8x8), B = df/du (8x4) row-major, xdot; and the mass matrix M(q) (4x4 row-major) */
+void oracle_exo_jac(const double* x, const double* u, double* A, double* B, double* xdot);
+void oracle_exo_mass(const double* q, double* M);
 /* linearised Euler step F_lin, ModelGenerator.cpp:47-48 (A,B row-major here) */
 void oracle_f_lin(int nx, int nu, double h, const double* A, const double* B, const double* x,
                   const double* u, const double* xdot_init, const double* x_init,
@@ -68,6 +72,9 @@ int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, con
 /* counter-based synthetic cfg#2 instances: splitmix64(seed, index) */
 void oracle_synth_two_link(uint64_t seed, int64_t first_index, int64_t B, int N, double h,
                            double* x0, double* u_prev, double* traj);
+/* counter-based synthetic cfg#3 (exo) instances */
+void oracle_synth_exo(uint64_t seed, int64_t first_index, int64_t B, int N, double h, double* x0,
+                      double* u_prev, double* traj);
 
 #ifdef __cplusplus
 }

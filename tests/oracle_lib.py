@@ -15,7 +15,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
 
-NX, NU = 4, 2
+NX, NU = 4, 2                       # 2-link arm (model 0)
+TWO_LINK, EXO = 0, 1
+DIMS = {TWO_LINK: (4, 2), EXO: (8, 4)}
 _lib = None
 
 _dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
@@ -43,6 +45,9 @@ def lib():
         ]
         L.oracle_solve_batch.restype = C.c_int
         L.oracle_synth_two_link.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int, C.c_double, _dp, _dp, _dp]
+        L.oracle_synth_exo.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int, C.c_double, _dp, _dp, _dp]
+        L.oracle_exo_jac.argtypes = [_dp, _dp, _dp, _dp, _dp]
+        L.oracle_exo_mass.argtypes = [_dp, _dp]
         _lib = L
     return _lib
 
@@ -57,6 +62,18 @@ def two_link_jac(x, u):
     return A.reshape(4, 4), B.reshape(4, 2), xd
 
 
+def exo_jac(x, u):
+    A = np.zeros(64); B = np.zeros(32); xd = np.zeros(8)
+    lib().oracle_exo_jac(c64(x), c64(u), A, B, xd)
+    return A.reshape(8, 8), B.reshape(8, 4), xd
+
+
+def exo_mass(q):
+    M = np.zeros(16)
+    lib().oracle_exo_mass(c64(q), M)
+    return M.reshape(4, 4)
+
+
 def f_lin(h, A, B, x, u, xdot_init, x_init, u_init):
     out = np.zeros(4)
     lib().oracle_f_lin(4, 2, h, c64(A).ravel(), c64(B).ravel(), c64(x), c64(u), c64(xdot_init),
@@ -64,27 +81,32 @@ def f_lin(h, A, B, x, u, xdot_init, x_init, u_init):
     return out
 
 
-def nlp_eval(N, h, V, u_prev, traj, weights):
-    J = np.zeros(1); g = np.zeros(N * NX)
-    lib().oracle_nlp_eval(0, N, h, c64(V), c64(u_prev), c64(traj).ravel(), c64(weights), J, g)
+def nlp_eval(N, h, V, u_prev, traj, weights, model=TWO_LINK):
+    nx, _ = DIMS[model]
+    J = np.zeros(1); g = np.zeros(N * nx)
+    lib().oracle_nlp_eval(model, N, h, c64(V), c64(u_prev), c64(traj).ravel(), c64(weights), J, g)
     return float(J[0]), g
 
 
-def reduced_gradient(N, h, x0, U, u_prev, traj, weights):
-    g = np.zeros(N * NU)
-    lib().oracle_reduced_gradient(0, N, h, c64(x0), c64(U).ravel(), c64(u_prev), c64(traj).ravel(),
+def reduced_gradient(N, h, x0, U, u_prev, traj, weights, model=TWO_LINK):
+    _, nu = DIMS[model]
+    g = np.zeros(N * nu)
+    lib().oracle_reduced_gradient(model, N, h, c64(x0), c64(U).ravel(), c64(u_prev), c64(traj).ravel(),
                                   c64(weights), g)
     return g
 
 
-def synth(seed, first, B, N, h):
-    x0 = np.zeros((B, NX)); up = np.zeros((B, NU)); tr = np.zeros((B, N, NX))
-    lib().oracle_synth_two_link(seed, first, B, N, h, x0.reshape(-1), up.reshape(-1), tr.reshape(-1))
+def synth(seed, first, B, N, h, model=TWO_LINK):
+    nx, nu = DIMS[model]
+    x0 = np.zeros((B, nx)); up = np.zeros((B, nu)); tr = np.zeros((B, N, nx))
+    fn = lib().oracle_synth_exo if model == EXO else lib().oracle_synth_two_link
+    fn(seed, first, B, N, h, x0.reshape(-1), up.reshape(-1), tr.reshape(-1))
     return x0, up, tr
 
 
 def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=50,
-                tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False):
+                tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK):
+    NX, NU = DIMS[model]
     x0 = c64(x0).reshape(-1, NX)
     B = x0.shape[0]
     NV = NX * (N + 1) + NU * N
@@ -95,7 +117,7 @@ def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, m
     lb = None if u_lb is None else c64(u_lb)
     ub = None if u_ub is None else c64(u_ub)
     rc = lib().oracle_solve_batch(
-        0, int(is_linear), N, h, B, x0.reshape(-1), c64(u_prev).reshape(-1), c64(traj).reshape(-1), weights.reshape(-1),
+        model, int(is_linear), N, h, B, x0.reshape(-1), c64(u_prev).reshape(-1), c64(traj).reshape(-1), weights.reshape(-1),
         w_stride, None if lb is None else lb.ctypes.data, None if ub is None else ub.ctypes.data,
         max_iter, tol_grad, tol_defect, V.reshape(-1), st, it, kkt, J, nthreads)
     assert rc == 0

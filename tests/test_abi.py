@@ -30,10 +30,11 @@ def test_library_is_gfx950_code_object(mmpc_mod):
 
 
 def test_abi_version_and_defaults(mmpc_mod):
-    assert mmpc_mod.lib().mmpc_abi_version() == 1
+    assert mmpc_mod.lib().mmpc_abi_version() == 2
     o = mmpc_mod.default_opts()
     assert o.max_iter == 50 and o.device == -1
     assert o.tol_grad == 1e-8 and o.tol_defect == 1e-10
+    assert o.kkt_solver == mmpc_mod.KKT_AUTO
 
 
 def test_load_model_json_like_reference(model_json, mmpc_mod):
@@ -65,7 +66,9 @@ def test_load_model_null_bounds_and_linear(tmp_path, mmpc_mod):
 @pytest.mark.parametrize("text,code", [
     ("{", -3),
     ('{"model": {"name": "x"}}', -3),
-    ('{"model": {"name": "x", "num_x": 8, "num_u": 4, "num_shooting_nodes": 50, "step_size": 2000}}', -4),
+    ('{"model": {"name": "x", "num_x": 6, "num_u": 3, "num_shooting_nodes": 50, "step_size": 2000}}', -4),
+    ('{"model": {"name": "x", "num_x": 4, "num_u": 2, "num_shooting_nodes": 10, "step_size": 2000,'
+     ' "mmpc_model": "exo_arm"}}', -3),
     ('{"model": {"name": "x", "num_x": 4, "num_u": 2, "num_shooting_nodes": 10, "step_size": 2000,'
      ' "mmpc_model": "nope"}}', -4),
     ('{"model": {"name": "x", "num_x": 4, "num_u": 2, "num_shooting_nodes": 10, "step_size": 2000,'
@@ -82,6 +85,27 @@ def test_missing_file_is_io_error(mmpc_mod, tmp_path):
     with pytest.raises(mmpc_mod.MmpcError) as ei:
         mmpc_mod.Solver(str(tmp_path / "nope.json"))
     assert ei.value.code == -2
+
+
+def test_load_exo_model(tmp_path, mmpc_mod):
+    # SURVEY.md 8a A3b / 8d cfg#3: nx=8 nu=4 N=50 resolves to the built-in exo by its dimensions
+    p = mmpc_mod.write_model_json(str(tmp_path / "exo.json"), "exo", 8, 4, 2000, 50)
+    s = mmpc_mod.Solver(p)
+    assert s.info.model_id == mmpc_mod.MODEL_EXO_ARM and s.NV == 8 * 51 + 4 * 50 == 608
+    s.close()
+    p = mmpc_mod.write_model_json(str(tmp_path / "exo2.json"), "exo2", 8, 4, 2000, 50, model="exo_arm")
+    assert mmpc_mod.Solver(p).info.model_id == mmpc_mod.MODEL_EXO_ARM
+
+
+def test_workspace_size_and_solver_choice(tmp_path, model_json, mmpc_mod):
+    # B = 0: size query only (no device needed); an unknown kkt_solver is rejected at creation
+    p = mmpc_mod.write_model_json(str(tmp_path / "exo.json"), "exo", 8, 4, 2000, 50)
+    s = mmpc_mod.Solver(p)
+    assert s.reserve_workspace(0) == 0
+    with pytest.raises(mmpc_mod.MmpcError):
+        s.reserve_workspace(-1)
+    with pytest.raises(mmpc_mod.MmpcError):
+        mmpc_mod.Solver(p, kkt_solver=7)
 
 
 def test_invalid_opts_rejected(model_json, mmpc_mod):
@@ -114,3 +138,7 @@ def test_flop_model(mmpc_mod):
     assert abs(mmpc_mod.survey_flops_per_iteration(30) - 288080) <= 1
     f = mmpc_mod.flops_per_iteration(30)
     assert f["total"] > 0 and f["gauss_jordan"] > f["hessian"] / 4
+    # cfg#3: 9,276,266 flop/iter condensed vs the Riccati recursion of the exo path
+    assert abs(mmpc_mod.survey_flops_per_iteration(50, 8, 4) - 9276266) <= 1
+    r = mmpc_mod.riccati_flops_per_iteration(50, 8, 4)
+    assert 0 < r["total"] < 9276266 / 30

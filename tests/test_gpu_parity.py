@@ -187,9 +187,11 @@ def test_horizons(N, model_json, mmpc_mod, oracle):
     _compare(r, o)
 
 
-def test_horizon_too_long_is_api_error(model_json, mmpc_mod, oracle):
+def test_horizon_too_long_for_condensed_is_api_error(model_json, mmpc_mod, oracle):
+    # N*nu > 64 does not fit the condensed kernel: an explicit request is an API error (no fallback);
+    # MMPC_KKT_AUTO routes it to the Riccati kernel (tests/test_gpu_riccati.py)
     x0, up, tr = oracle.synth(5, 0, 2, 33, H)
-    s = mmpc_mod.Solver(model_json(N=33))
+    s = mmpc_mod.Solver(model_json(N=33), kkt_solver=mmpc_mod.KKT_CONDENSED)
     with pytest.raises(mmpc_mod.MmpcError) as ei:
         s.solve_batch_host(x0, up, tr, np.array(WEIGHTS_CFG))
     assert ei.value.code == -4

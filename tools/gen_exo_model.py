@@ -1,0 +1,336 @@
+#!/usr/bin/env python3
+"""Generate the exo mass-matrix code and its known-answer fixture (run in the build container only).
+
+The reference's only exo dynamics artefact is the symbolic 4x4 mass matrix M(q) printed by CasADi in
+src/inverseTest.cpp:59-74.  This script
+
+  1. parses the ten upper-triangle entries M00..M33 of that file (as math, with sympy),
+  2. substitutes the build-defined inertial parameters of tests/golden/exo_params.json (exact rationals),
+  3. rewrites each entry as a polynomial in c_i = cos q_i, s_i = sin q_i (i = 1..3; M does not depend on q0),
+     where the printout's symbols q1..q3 are joints 1..3 of the 0-based state [q0..q3, qd0..qd3]
+     (util/testCorrectEquations.py:16-23); q0 is the base joint,
+  4. emits
+       mahi-mpc_amd/csrc/exo_model_gen.h  device functions mass_upper / dmass_upper<J> (sums of monomials over
+                                          a table of trig powers, derivatives symbolic)
+       oracle/exo_model_gen.h             C function      exo_mass_and_grad(q, M[16], dM[4][16])
+                                          with the partial derivatives taken symbolically (independent of
+                                          the device's forward-mode duals)
+       tests/golden/exo_mass_kat.json     M(q) at fixed q evaluated from the *unexpanded* parsed expressions
+                                          with 40-digit mpmath -- the pin for both generated forms.
+
+/root/reference exists only in this container; the generated files are committed and nothing reads the
+reference at build or run time.  Re-run after changing exo_params.json:
+    python tools/gen_exo_model.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import re
+import sys
+
+import mpmath
+import sympy as sp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = "/root/reference/src/inverseTest.cpp"
+UPPER = ["M00", "M01", "M02", "M03", "M11", "M12", "M13", "M22", "M23", "M33"]
+IDX = [(0, 0), (0, 1), (0, 2), (0, 3), (1, 1), (1, 2), (1, 3), (2, 2), (2, 3), (3, 3)]
+
+
+def load_entries():
+    text = open(REF).read()
+    ents = dict(re.findall(r"casadi::SX (M\d\d) = (.*?);", text))
+    q = sp.symbols("q1 q2 q3 q4")
+    params = {}
+    for base in ["Icxx", "Icyy", "Iczz", "Icxy", "Icxz", "Icyz", "Pcx", "Pcy", "Pcz", "m"]:
+        for i in range(4):
+            params[f"{base}{i}"] = sp.Symbol(f"{base}{i}")
+    loc = dict(params)
+    loc.update({"q1": q[0], "q2": q[1], "q3": q[2], "q4": q[3], "cos": sp.cos, "sin": sp.sin,
+                "pow": lambda a, b: a ** b, "Rational": sp.Rational})
+    out = {}
+    for k in UPPER:
+        e = re.sub(r"(\d+\.\d+(?:E[+-]\d+)?)", r"Rational('\1')", ents[k])
+        out[k] = sp.sympify(e, locals=loc)
+    # symmetry of the printout
+    for a in range(4):
+        for b in range(a):
+            e = re.sub(r"(\d+\.\d+(?:E[+-]\d+)?)", r"Rational('\1')", ents[f"M{a}{b}"])
+            lower = sp.sympify(e, locals=loc)
+            assert sp.simplify(lower - out[f"M{b}{a}"]) == 0, f"M{a}{b} != M{b}{a}"
+    return out, q, params
+
+
+def param_subs(params, pj):
+    subs = {}
+    for base in ["Icxx", "Icyy", "Iczz", "Icxy", "Icxz", "Icyz", "Pcx", "Pcy", "Pcz", "m"]:
+        for i in range(4):
+            subs[params[f"{base}{i}"]] = sp.Rational(pj[base][i])
+    return subs
+
+
+class TPrinter:
+    """Prints a sympy polynomial expression over a generic scalar type (only +, -, *, double literals)."""
+
+    def __init__(self, num_fmt):
+        self.num_fmt = num_fmt
+
+    def p(self, e):
+        if e.is_Symbol:
+            return str(e)
+        if e.is_Number:
+            return self.num_fmt(float(e))
+        if e.is_Add:
+            terms = [self.p(a) for a in e.args]
+            s = terms[0]
+            for t in terms[1:]:
+                s = f"{s} - {t[1:]}" if t.startswith("-") else f"{s} + {t}"
+            return f"({s})"
+        if e.is_Mul:
+            coef, rest = e.as_coeff_Mul()
+            factors = []
+            for f in sp.Mul.make_args(rest):
+                if f.is_Pow:
+                    base, ex = f.args
+                    assert ex.is_Integer and ex > 0, f
+                    factors += [self.p(base)] * int(ex)
+                else:
+                    factors.append(self.p(f))
+            body = " * ".join(factors)
+            if coef == 1:
+                return body
+            if coef == -1:
+                return f"-({body})" if len(factors) > 1 else f"-{body}"
+            return f"{self.num_fmt(float(coef))} * {body}"
+        if e.is_Pow:
+            base, ex = e.args
+            assert ex.is_Integer and ex > 0, e
+            return "(" + " * ".join([self.p(base)] * int(ex)) + ")"
+        raise ValueError(f"unsupported node {e!r}")
+
+
+def lit(x):
+    r = repr(float(x))
+    return r if ("e" in r or "." in r or "inf" in r) else r + ".0"
+
+
+def main():
+    pj = json.load(open(os.path.join(REPO, "tests", "golden", "exo_params.json")))
+    ents, q, params = load_entries()
+    subs = param_subs(params, pj)
+    c = sp.symbols("c1 c2 c3")
+    s = sp.symbols("s1 s2 s3")
+    trig = {}
+    for i in range(3):
+        trig[sp.cos(q[i])] = c[i]
+        trig[sp.sin(q[i])] = s[i]
+    polys = []
+    for k in UPPER:
+        e = sp.expand_trig(ents[k].subs(subs))
+        e = sp.expand(e.subs(trig))
+        assert not e.has(sp.sin) and not e.has(sp.cos), k
+        polys.append(e)
+    nterms = sum(len(sp.Add.make_args(p)) for p in polys)
+
+    # ---- device code: M and dM/dq_j as sums of monomials over a table of trig powers ----
+    # (no cross-entry CSE: every output is an independent fma chain, so few values are live at once)
+    gens = list(c) + list(s)
+    names = ["c1", "c2", "c3", "s1", "s2", "s3"]
+    dpolys = []
+    for j in range(3):
+        dpolys.append([sp.expand(-s[j] * sp.diff(pe, c[j]) + c[j] * sp.diff(pe, s[j])) for pe in polys])
+    used = set()
+
+    coefs = []
+    cindex = {}
+
+    def cref(v):
+        # every non-trivial coefficient lives in one __constant__ table: f64 literals cannot be encoded in
+        # VALU instructions, and as immediates the compiler hoists all of them out of the solver loops
+        # and spills them; table entries are scalar-loaded at their point of use
+        if v not in cindex:
+            cindex[v] = len(coefs)
+            coefs.append(v)
+        return f"K[{cindex[v]}]"
+
+    def emit_poly(pe):
+        terms = sp.Poly(pe, *gens).terms()
+        const = 0.0
+        parts = []
+        for mon, coef in terms:
+            if all(e == 0 for e in mon):
+                const = float(coef)
+                continue
+            fac = []
+            for v, e in zip(names, mon):
+                if e == 1:
+                    fac.append(v)
+                elif e > 1:
+                    fac.append(f"{v}_{e}")
+                    used.add((v, e))
+            parts.append((float(coef), " * ".join(fac)))
+        expr = cref(const) if const != 0.0 else "0.0"
+        for coef, mono in parts:
+            expr = f"fma({cref(coef)}, {mono}, {expr})"
+        return expr, len(parts)
+
+    mlines, nmono = [], 0
+    for i, pe in enumerate(polys):
+        e, n = emit_poly(pe)
+        nmono += n
+        mlines.append(f"    M[{i}] = {e};")
+    dlines, ndmono = [], 0
+    for j in range(3):
+        dlines.append(f"    if (J == {j + 1}) {{")
+        for i, pe in enumerate(dpolys[j]):
+            e, n = emit_poly(pe)
+            ndmono += n
+            dlines.append(f"        dM[{i}] = {e};")
+        dlines.append("    }")
+    pw = []
+    for v, e in sorted(used):
+        pw.append(f"        {v}_{e} = " + " * ".join([v] * e) + ";")
+    pw_decl = ", ".join(f"{v}_{e}" for v, e in sorted(used))
+    unpack = ", ".join(f"{v}_{e} = t.{v}_{e}" for v, e in sorted(used))
+    dev = f"""// exo_model_gen.h -- GENERATED by tools/gen_exo_model.py; do not edit.
+//
+// Mass matrix M(q) of the 4-DoF exo, restated from the CasADi printout of src/inverseTest.cpp:59-74
+// with the build-defined inertial parameters of tests/golden/exo_params.json substituted (NOT
+// reference-pinned values; the reference ships none), as polynomials in c_i = cos q_i, s_i = sin q_i
+// (i = 1..3; M does not depend on q0): {nmono} monomials for M, {ndmono} for dM/dq_1..3 (symbolic
+// derivatives).  Outputs are the upper triangle M00 M01 M02 M03 M11 M12 M13 M22 M23 M33.
+#pragma once
+
+namespace mmpc {{
+namespace exo {{
+
+constexpr double kGravityGain[4] = {{{", ".join(lit(sp.Rational(v)) for v in pj["gravity_gain"])}}};
+constexpr double kDamping[4] = {{{", ".join(lit(sp.Rational(v)) for v in pj["damping"])}}};
+
+// the {len(coefs)} distinct polynomial coefficients
+__constant__ double kCoef[{len(coefs)}] = {{{", ".join(lit(v) for v in coefs)}}};
+
+// table pointer made opaque per call: the loads stay at their uses (no loop-invariant hoisting)
+__device__ __forceinline__ const double* coef_table() {{
+    const double* K = kCoef;
+    asm volatile("" : "+s"(K));
+    return K;
+}}
+
+struct TrigPowers {{
+    double c1, c2, c3, s1, s2, s3;
+    double {pw_decl};
+    __device__ __forceinline__ TrigPowers(double c1_, double c2_, double c3_, double s1_, double s2_, double s3_)
+        : c1(c1_), c2(c2_), c3(c3_), s1(s1_), s2(s2_), s3(s3_) {{
+{chr(10).join(pw)}
+    }}
+}};
+
+__device__ __forceinline__ void mass_upper(const TrigPowers& t, double* M) {{
+    const double* K = coef_table();
+    [[maybe_unused]] const double c1 = t.c1, c2 = t.c2, c3 = t.c3, s1 = t.s1, s2 = t.s2, s3 = t.s3;
+    [[maybe_unused]] const double {unpack};
+{chr(10).join(mlines)}
+}}
+
+// dM/dq_J (J = 1..3), upper triangle
+template <int J>
+__device__ __forceinline__ void dmass_upper(const TrigPowers& t, double* dM) {{
+    const double* K = coef_table();
+    [[maybe_unused]] const double c1 = t.c1, c2 = t.c2, c3 = t.c3, s1 = t.s1, s2 = t.s2, s3 = t.s3;
+    [[maybe_unused]] const double {unpack};
+{chr(10).join(dlines)}
+}}
+
+}}  // namespace exo
+}}  // namespace mmpc
+"""
+    open(os.path.join(REPO, "mahi-mpc_amd", "csrc", "exo_model_gen.h"), "w").write(dev)
+    repl = []
+    P = TPrinter(lit)
+
+    # ---- oracle: M and dM/dq_j by symbolic differentiation ----
+    exprs = []
+    for pexpr in polys:
+        exprs.append(pexpr)
+    for j in range(3):
+        for pexpr in polys:
+            d = -s[j] * sp.diff(pexpr, c[j]) + c[j] * sp.diff(pexpr, s[j])
+            exprs.append(sp.expand(d))
+    repl2, red2 = sp.cse(exprs, symbols=sp.numbered_symbols("t"), optimizations="basic")
+    ol = []
+    for sym, ex in repl2:
+        ol.append(f"    const double {sym} = {P.p(ex)};")
+    for i, ex in enumerate(red2):
+        ol.append(f"    up[{i}] = {P.p(ex)};")
+    orc = f"""/* exo_model_gen.h -- GENERATED by tools/gen_exo_model.py; do not edit.
+ *
+ * TEST INFRASTRUCTURE (oracle).  M(q) of src/inverseTest.cpp:59-74 with the build-defined parameters of
+ * tests/golden/exo_params.json, and its partial derivatives dM/dq_j taken symbolically (sympy), i.e.
+ * independently of the device's forward-mode dual numbers.
+ */
+#ifndef MMPC_EXO_MODEL_GEN_H
+#define MMPC_EXO_MODEL_GEN_H
+#include <math.h>
+
+static const double EXO_GRAVITY_GAIN[4] = {{{", ".join(lit(sp.Rational(v)) for v in pj["gravity_gain"])}}};
+static const double EXO_DAMPING[4] = {{{", ".join(lit(sp.Rational(v)) for v in pj["damping"])}}};
+
+/* M[16] row-major, dM[j][16] = dM/dq_j (dM[0] = 0: M does not depend on q0) */
+static void exo_mass_and_grad(const double* q, double* M, double dM[4][16]) {{
+    const double c1 = cos(q[1]), s1 = sin(q[1]), c2 = cos(q[2]), s2 = sin(q[2]), c3 = cos(q[3]), s3 = sin(q[3]);
+    double up[40];
+{chr(10).join(ol)}
+    static const int ia[10] = {{0, 0, 0, 0, 1, 1, 1, 2, 2, 3}}, ib[10] = {{0, 1, 2, 3, 1, 2, 3, 2, 3, 3}};
+    for (int j = 0; j < 16; ++j) dM[0][j] = 0.0;
+    for (int t = 0; t < 10; ++t) {{
+        M[ia[t] * 4 + ib[t]] = M[ib[t] * 4 + ia[t]] = up[t];
+        for (int j = 0; j < 3; ++j) dM[j + 1][ia[t] * 4 + ib[t]] = dM[j + 1][ib[t] * 4 + ia[t]] = up[10 + 10 * j + t];
+    }}
+}}
+#endif
+"""
+    open(os.path.join(REPO, "oracle", "exo_model_gen.h"), "w").write(orc)
+
+    # ---- known-answer fixture from the unexpanded expressions (40 digits) ----
+    mpmath.mp.dps = 40
+    pts = [[0.0, 0.0, 0.0, 0.0], [0.1, 0.3, -0.2, 0.4], [-0.5, 0.5, 0.5, -0.5], [1.0, -1.2, 0.7, 2.0],
+           [0.0, 3.0, -2.5, 1.5], [0.2, 1.5707963267948966, 0.0, -1.5707963267948966]]
+    import random
+    rng = random.Random(20250213)
+    for _ in range(6):
+        pts.append([rng.uniform(-3.14, 3.14) for _ in range(4)])
+    kat = []
+    for qq in pts:
+        # printout symbol q_k (k = 1..3) is joint k of the 0-based state [q0..q3] (q0 = base joint, on which
+        # M of a serial chain cannot depend; q4 is declared but unused at inverseTest.cpp:11)
+        vals = {q[i]: sp.Float(repr(qq[i + 1]), 40) for i in range(3)}
+        M = [[0.0] * 4 for _ in range(4)]
+        for (a, b), k in zip(IDX, UPPER):
+            v = sp.N(ents[k].subs(subs).subs(vals), 40)
+            M[a][b] = M[b][a] = float(v)
+        kat.append({"q": qq, "M": M})
+    # positive definiteness over a grid (the parameters must be physically consistent)
+    import numpy as np
+    f = sp.lambdify((c, s), polys, "numpy")
+    worst = np.inf
+    for _ in range(2000):
+        qq = np.array([rng.uniform(-np.pi, np.pi) for _ in range(3)])
+        up = f(np.cos(qq), np.sin(qq))
+        Mn = np.zeros((4, 4))
+        for (a, b), v in zip(IDX, up):
+            Mn[a, b] = Mn[b, a] = v
+        worst = min(worst, np.linalg.eigvalsh(Mn)[0])
+    assert worst > 0, f"M(q) not positive definite (min eig {worst})"
+    json.dump({"source": "src/inverseTest.cpp:59-74 (CasADi printout of M(q)), parameters tests/golden/exo_params.json",
+               "method": "sympy parse of the printed expressions, evaluated with 40-digit mpmath, no expansion",
+               "min_eigenvalue_over_2000_random_q": worst, "monomials": nterms, "cases": kat},
+              open(os.path.join(REPO, "tests", "golden", "exo_mass_kat.json"), "w"), indent=1)
+    print(f"monomials {nterms} (M) / {ndmono} (dM), oracle cse temps {len(repl2)}, min eig {worst:.3e}")
+
+
+if __name__ == "__main__":
+    if not os.path.exists(REF):
+        sys.exit(f"{REF} not found: the generator runs only in the build container")
+    main()
