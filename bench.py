@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
-                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py), if present")
+                    help="PMC-derived HBM bytes per launch per config (tools/pmc.sh + tools/pmc_summary.py)")
     return ap.parse_args()
 
 
@@ -172,12 +172,11 @@ def main():
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("batch") == B and tj.get("horizon") == N and tj.get("config", "cfg2") == args.config:
+            tj = json.load(open(args.traffic_json)).get(args.config, {})
+            if tj.get("batch") == B and tj.get("horizon") == N:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-
     out = {
         "metric": cfg["metric"],
         "value": value,

@@ -102,6 +102,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NS = NX + NU, ND = NX + NU;
     static_assert(NX == 2 * NQ, "second-order models only (x = [q; qd])");
     const int64_t inst = blockIdx.x * (int64_t)64 + threadIdx.x;
+    const int lane0 = threadIdx.x;
+    MMPC_PHASE_DECL
     // Riccati matrix P~ (packed upper, NS(NS+1)/2 doubles per lane) lives in LDS, lane-interleaved
     // (conflict-free): holding it in registers next to the stage blocks and the factor spills to scratch.
     __shared__ double sP[NS * (NS + 1) / 2][64];
@@ -218,28 +220,41 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     int status = ST_MAX_ITER;
     int it = 0;
     double kkt = 0.0, mu = 0.0;
+    MMPC_PHASE(0);
     #pragma unroll 1
     for (it = 0; it <= p.max_iter; ++it) {
         // ---- (1) forward: F, defects, d_{k+1} = A_k d_k + c_k, merit value ----
         double J0 = 0.0, c1 = 0.0, cmax = 0.0;
         bool nonfinite = false;
         {
-            double d[NX], xk[NX], um[NU];
+            // software pipeline: the model inputs of stage k+1 are loaded during stage k (one wave per SIMD
+            // has no other wave to hide HBM latency behind); the other loads of a stage are issued before
+            // its model evaluation, which covers them
+            double d[NX], xk[NX], um[NU], un[NU];
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 d[r] = 0.0;
                 xk[r] = ST(0, SF::X, r);
             }
 #pragma unroll
-            for (int c = 0; c < NU; ++c) um[c] = up[c];
+            for (int c = 0; c < NU; ++c) {
+                um[c] = up[c];
+                un[c] = ST(0, SF::U, c);
+            }
             #pragma unroll 1
             for (int k = 0; k < N; ++k) {
                 double* const sk = stage_ptr(wsb, k, SS, lane);
-                double u[NU], xn[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+                double u[NU], xn[NX], rk[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
 #pragma unroll
-                for (int c = 0; c < NU; ++c) u[c] = SK(0, SF::U, c);
+                for (int c = 0; c < NU; ++c) {
+                    u[c] = un[c];
+                    un[c] = SK(1, SF::U, c);  // stage N's U slot exists (unused) when k = N-1
+                }
 #pragma unroll
-                for (int r = 0; r < NX; ++r) xn[r] = SK(1, SF::X, r);
+                for (int r = 0; r < NX; ++r) {
+                    xn[r] = SK(1, SF::X, r);
+                    rk[r] = SK(0, SF::R, r);
+                }
                 STAGE_EVAL(xk, u, xd, hFq, hFqd, hFu, true);
                 double dn[NX];
                 a_mul<NQ>(h, hFq, hFqd, d, dn);
@@ -251,7 +266,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     cmax = fmax(cmax, fabs(c));
                     c1 += fabs(c);
                     nonfinite |= !isfinite(c);
-                    const double e = F - SK(0, SF::R, r);
+                    const double e = F - rk[r];
                     J0 = fma(e * Q[r], e, J0);
                     d[r] = dn[r] + c;
                     SK(1, SF::D, r) = d[r];
@@ -266,6 +281,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             }
         }
 
+        MMPC_PHASE(1);
         // ---- (2) backward: adjoint + reduced gradient (stopping test) and the Riccati recursion ----
         // Value function V_k(s) = s^T P s + 2 p^T s on s = [dx_k; du_{k-1}] (no 1/2: J has none,
         // ModelGenerator.cpp:208-222); (P, pv) hold P~_{k+1} = P_{k+1} + blkdiag(Q, 0) on entry to step k.
@@ -286,22 +302,45 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 lam[r] = Q[r] * (ST(N, SF::D, r) + eb);  // lam_N = Q e_{N-1}
                 lmax = fmax(lmax, fabs(lam[r]));
             }
+            // software pipeline as in (1): x_{k-1}, u_{k-1} (model inputs of the next step) are loaded during
+            // step k, everything else of step k before its model evaluation
+            double xpf[NX], upf[NU];
 #pragma unroll
-            for (int c = 0; c < NU; ++c) unext[c] = 0.0;
+            for (int c = 0; c < NU; ++c) {
+                unext[c] = 0.0;
+                upf[c] = ST(N - 1, SF::U, c);
+            }
+#pragma unroll
+            for (int r = 0; r < NX; ++r) xpf[r] = ST(N - 1, SF::X, r);
             #pragma unroll 1
             for (int k = N - 1; k >= 0; --k) {
                 double* const sk = stage_ptr(wsb, k, SS, lane);
-                double x[NX], u[NU], um[NU], cc[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+                double x[NX], u[NU], um[NU], cc[NX], dk[NX], rkm[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ],
+                    hFu[NQ * NU];
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
-                    x[r] = SK(0, SF::X, r);
+                    x[r] = xpf[r];
                     cc[r] = SK(0, SF::C, r);
+                    dk[r] = SK(0, SF::D, r);
                 }
 #pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    u[c] = SK(0, SF::U, c);
-                    um[c] = (k == 0) ? up[c] : SK(-1, SF::U, c);
+                for (int c = 0; c < NU; ++c) u[c] = upf[c];
+                if (k >= 1) {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        rkm[r] = SK(-1, SF::R, r);
+                        xpf[r] = SK(-1, SF::X, r);
+                    }
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) um[c] = SK(-1, SF::U, c);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) rkm[r] = 0.0;
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) um[c] = up[c];
                 }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) upf[c] = um[c];
                 STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
                 // reduced gradient g_k = B_k^T lam_{k+1} + R/Rm terms (same expression as sqp_wave.h)
 #pragma unroll
@@ -321,7 +360,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     at_mul<NQ>(h, hFq, hFqd, lam, ln);
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
-                        lam[r] = fma(Q[r], SK(0, SF::D, r) + x[r] - SK(-1, SF::R, r), ln[r]);
+                        lam[r] = fma(Q[r], dk[r] + x[r] - rkm[r], ln[r]);
                         lmax = fmax(lmax, fabs(lam[r]));
                     }
                 }
@@ -387,7 +426,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     double t[NX];
                     at_mul<NQ>(h, hFq, hFqd, mv, t);
 #pragma unroll
-                    for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - SK(-1, SF::R, q), t[q]);
+                    for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - rkm[q], t[q]);
 #pragma unroll
                     for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
                 }
@@ -469,6 +508,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 }
             }
         }
+        MMPC_PHASE(2);
         kkt = fmax(gmax, cmax);
         // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
         double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
@@ -510,15 +550,29 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 dup[c] = 0.0;
                 um[c] = up[c];
             }
+            // software pipeline as in (1); the feedback gains K_k are consumed (and loaded) before the model
+            // evaluation, whose compute then covers the remaining loads of the stage
+            double xpf[NX], upf[NU];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) xpf[r] = ST(0, SF::X, r);
+#pragma unroll
+            for (int c = 0; c < NU; ++c) upf[c] = ST(0, SF::U, c);
             #pragma unroll 1
             for (int k = 0; k < N; ++k) {
                 double* const sk = stage_ptr(wsb, k, SS, lane);
-                double x[NX], u[NU], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+                double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
 #pragma unroll
-                for (int r = 0; r < NX; ++r) x[r] = SK(0, SF::X, r);
+                for (int r = 0; r < NX; ++r) {
+                    x[r] = xpf[r];
+                    xpf[r] = SK(1, SF::X, r);
+                    rk[r] = SK(0, SF::R, r);
+                    ck[r] = SK(0, SF::C, r);
+                }
 #pragma unroll
-                for (int c = 0; c < NU; ++c) u[c] = SK(0, SF::U, c);
-                STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                for (int c = 0; c < NU; ++c) {
+                    u[c] = upf[c];
+                    upf[c] = SK(1, SF::U, c);  // stage N's U slot exists (unused) when k = N-1
+                }
                 double du[NU];
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
@@ -531,6 +585,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     du[a] = t;
                     SK(0, SF::DU, a) = t;
                 }
+                STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
                 double ad[NX];
                 a_mul<NQ>(h, hFq, hFqd, dx, ad);
 #pragma unroll
@@ -540,9 +595,9 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
                     const double F = fma(h, xd[r], x[r]);
-                    const double qe = 2.0 * Q[r] * (F - SK(0, SF::R, r));
+                    const double qe = 2.0 * Q[r] * (F - rk[r]);
                     dJ = fma(qe, ad[r], dJ);
-                    dx[r] = ad[r] + SK(0, SF::C, r);
+                    dx[r] = ad[r] + ck[r];
                     SK(1, SF::DX, r) = dx[r];
                 }
 #pragma unroll
@@ -555,6 +610,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             }
         }
 
+        MMPC_PHASE(4);
         // ---- (4) l1-merit Armijo line search (noise-aware, as sqp_wave.h) ----
         mu = fmax(mu, 4.0 * lmax + 1.0);
         const double phi0 = fma(mu, c1, J0);
@@ -563,19 +619,30 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         bool accepted = false;
         #pragma unroll 1
         for (int ls = 0; ls < 30; ++ls) {
-            double Jt = 0.0, ct = 0.0, xk[NX], umt[NU];
+            double Jt = 0.0, ct = 0.0, xk[NX], umt[NU], upf[NU], dupf[NU];
 #pragma unroll
             for (int r = 0; r < NX; ++r) xk[r] = ST(0, SF::X, r);  // dx_0 = 0
 #pragma unroll
-            for (int c = 0; c < NU; ++c) umt[c] = up[c];
+            for (int c = 0; c < NU; ++c) {
+                umt[c] = up[c];
+                upf[c] = ST(0, SF::U, c);
+                dupf[c] = ST(0, SF::DU, c);
+            }
             #pragma unroll 1
             for (int k = 0; k < N; ++k) {
                 double* const sk = stage_ptr(wsb, k, SS, lane);
-                double u[NU], xn[NX], xd[NX];
+                double u[NU], xn[NX], xd[NX], rk[NX];
 #pragma unroll
-                for (int c = 0; c < NU; ++c) u[c] = fma(alpha, SK(0, SF::DU, c), SK(0, SF::U, c));
+                for (int c = 0; c < NU; ++c) {
+                    u[c] = fma(alpha, dupf[c], upf[c]);
+                    upf[c] = SK(1, SF::U, c);   // software pipeline as in (1)
+                    dupf[c] = SK(1, SF::DU, c);
+                }
 #pragma unroll
-                for (int r = 0; r < NX; ++r) xn[r] = fma(alpha, SK(1, SF::DX, r), SK(1, SF::X, r));
+                for (int r = 0; r < NX; ++r) {
+                    xn[r] = fma(alpha, SK(1, SF::DX, r), SK(1, SF::X, r));
+                    rk[r] = SK(0, SF::R, r);
+                }
                 {
                     double* nil_ = nullptr;
                     STAGE_EVAL(xk, u, xd, nil_, nil_, nil_, false);
@@ -583,7 +650,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
                     const double F = fma(h, xd[r], xk[r]);
-                    const double er = F - SK(0, SF::R, r);
+                    const double er = F - rk[r];
                     Jt = fma(er * Q[r], er, Jt);
                     ct += fabs(F - xn[r]);
                     xk[r] = xn[r];
@@ -603,6 +670,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             }
             alpha *= 0.5;
         }
+        MMPC_PHASE(5);
         if (trc) {
             trc[4] = dJ;
             trc[5] = alpha;
@@ -626,6 +694,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         }
     }
 
+    MMPC_PHASE(6);
     // ---- bounds check (box constraints are reported, not yet enforced), as sqp_wave.h ----
     if (status == ST_CONVERGED && (p.u_lb || p.u_ub)) {
         bool viol = false;
@@ -651,6 +720,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     if (p.status) p.status[inst] = status;
     if (p.iters) p.iters[inst] = it;
     if (p.kkt) p.kkt[inst] = kkt;
+    MMPC_PHASE(7);
+    MMPC_PHASE_FLUSH
 #undef ST
 #undef SK
 #undef PS

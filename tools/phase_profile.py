@@ -19,19 +19,28 @@ import mmpc  # noqa: E402
 
 NAMES = ["load", "stage_eval", "d_forward", "adjoint+grad+check", "lyapunov", "hessian", "gauss_jordan",
          "dx_forward", "line_search", "writeback"]
+NAMES_LANE = ["load", "forward(F,c,d)", "backward(grad+riccati)", "-", "check+forward(step)", "line_search",
+              "after_loop", "writeback", "-", "-"]
 ap = argparse.ArgumentParser()
-ap.add_argument("--batch", type=int, default=4096)
-ap.add_argument("--horizon", type=int, default=30)
+ap.add_argument("--config", choices=["cfg2", "cfg3"], default="cfg2")
+ap.add_argument("--batch", type=int, default=None)
+ap.add_argument("--horizon", type=int, default=None)
+ap.add_argument("--kkt", type=int, default=0, help="kkt_solver (0 auto, 1 condensed, 2 riccati)")
 a = ap.parse_args()
-B, N = a.batch, a.horizon
+exo = a.config == "cfg3"
+B = a.batch or (65536 if exo else 4096)
+N = a.horizon or (50 if exo else 30)
+nx, nu = (8, 4) if exo else (4, 2)
 L = mmpc.lib()
 L.mmpc_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
-path = mmpc.write_model_json("/tmp/mmpc_phase.json", "nonlinear_double_pendulum", 4, 2, 2000, N)
-s = mmpc.Solver(path)
+path = mmpc.write_model_json("/tmp/mmpc_phase.json", "phase", nx, nu, 2000, N)
+s = mmpc.Solver(path, kkt_solver=a.kkt)
+if exo or a.kkt == 2 or N * nu > 64:
+    NAMES = NAMES_LANE
 f = dict(dtype=torch.float64, device="cuda")
-x0 = torch.empty((B, 4), **f); up = torch.empty((B, 2), **f); tr = torch.empty((B, N, 4), **f)
+x0 = torch.empty((B, nx), **f); up = torch.empty((B, nu), **f); tr = torch.empty((B, N, nx), **f)
 s.synth(20250213, 0, B, x0, up, tr)
-w = torch.tensor([10, 1, 5, 5, 5, 5, .01, .01], **f)
+w = torch.tensor([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4 if exo else [10, 1, 5, 5, 5, 5, .01, .01], **f)
 V = torch.zeros((B, s.NV), **f)
 it = torch.zeros(B, dtype=torch.int32, device="cuda")
 s.solve_batch(B, x0, up, tr, w, V, None, it, None)
@@ -45,7 +54,7 @@ L.mmpc_debug_phase_cycles(buf, 1)
 cyc = np.array(buf[:10], dtype=np.float64)
 waves = buf[15]
 iters = it.cpu().numpy()
-out = {"waves": int(waves), "mean_iters": float(iters.mean()),
+out = {"config": a.config, "waves": int(waves), "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
        "cycles_per_wave": float(cyc.sum() / waves),
        "per_phase_cycles_per_wave_iteration": {n: float(c / waves / (iters.mean() + 1)) for n, c in zip(NAMES, cyc)},
        "share": {n: float(c / cyc.sum()) for n, c in zip(NAMES, cyc)}}

@@ -10,15 +10,16 @@ import sys
 from collections import defaultdict
 
 out = sys.argv[1]
+kname = sys.argv[2] if len(sys.argv) > 2 else "sqp_wave_kernel"
 vals = defaultdict(list)
 for f in glob.glob(os.path.join(out, "*", "**", "*counter_collection.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
-        if "sqp_wave_kernel" not in row.get("Kernel_Name", ""):
+        if kname not in row.get("Kernel_Name", ""):
             continue
         vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
 # counters are reported per dispatch (summed over dimensions by rocprofv3 v3 csv: one row per dispatch+counter)
 summary = {k: sum(v) / len(v) for k, v in vals.items()}
-res = {"per_dispatch_mean": summary}
+res = {"kernel": kname, "per_dispatch_mean": summary}
 if "FETCH_SIZE" in summary and "WRITE_SIZE" in summary:
     fetch_b = summary["FETCH_SIZE"] * 1024 * 2.0
     write_b = summary["WRITE_SIZE"] * 1024
