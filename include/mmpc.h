@@ -104,7 +104,8 @@ typedef struct mmpc_opts {
     double tol_grad;    /* ||grad_u J_reduced||_inf stop tolerance. default 1e-8 */
     double tol_defect;  /* ||g||_inf stop tolerance. default 1e-10 */
     int32_t kkt_solver; /* enum mmpc_kkt_solver. default MMPC_KKT_AUTO */
-    int32_t reserved;
+    int32_t factor_fp32; /* 1: Riccati factor/solve in fp32, residuals/merit/iterates in fp64 (SURVEY 8d
+                            cfg#5; each SQP iteration refines the fp32 step). Riccati solver only. default 0 */
 } mmpc_opts;
 
 typedef struct mmpc_model_info {

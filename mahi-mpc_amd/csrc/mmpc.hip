@@ -167,6 +167,7 @@ int validate_opts(const mmpc_opts* o) {
     if (!(o->tol_grad > 0.0) || !(o->tol_defect > 0.0)) return fail(MMPC_ERR_INVALID_ARG, "tolerances must be > 0");
     if (o->kkt_solver < MMPC_KKT_AUTO || o->kkt_solver > MMPC_KKT_RICCATI)
         return fail(MMPC_ERR_INVALID_ARG, "unknown kkt_solver");
+    if (o->factor_fp32 != 0 && o->factor_fp32 != 1) return fail(MMPC_ERR_INVALID_ARG, "factor_fp32 must be 0 or 1");
     return MMPC_OK;
 }
 
@@ -401,8 +402,10 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     const int N = mi.num_shooting_nodes;
     int solver = h->opts.kkt_solver;
     const bool condensed_ok = mi.model_id == MMPC_MODEL_TWO_LINK_ARM && N * TwoLinkArm::NU <= 64;
-    if (solver == MMPC_KKT_AUTO) solver = condensed_ok ? MMPC_KKT_CONDENSED : MMPC_KKT_RICCATI;
+    if (solver == MMPC_KKT_AUTO)
+        solver = (condensed_ok && !h->opts.factor_fp32) ? MMPC_KKT_CONDENSED : MMPC_KKT_RICCATI;
     if (solver == MMPC_KKT_CONDENSED) {
+        if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 is a Riccati-solver option");
         // host-side shape checks: the kernel holds one condensed-Hessian row per lane
         if (!condensed_ok)
             return fail(MMPC_ERR_UNSUPPORTED, "condensed solver needs the 2-link arm and N*nu <= 64");
@@ -415,8 +418,14 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
         int rc = ensure_workspace(h, B, &lw);
         if (rc) return rc;
         dim3 grid(grid1d(B, 64)), block(64);
-        if (mi.model_id == MMPC_MODEL_EXO_ARM) sqp_lane_kernel<ExoArm><<<grid, block, 0, stream>>>(p, lw);
-        else sqp_lane_kernel<TwoLinkArm><<<grid, block, 0, stream>>>(p, lw);
+        const bool f32 = h->opts.factor_fp32 != 0;
+        if (mi.model_id == MMPC_MODEL_EXO_ARM) {
+            if (f32) sqp_lane_kernel<ExoArm, float><<<grid, block, 0, stream>>>(p, lw);
+            else sqp_lane_kernel<ExoArm, double><<<grid, block, 0, stream>>>(p, lw);
+        } else {
+            if (f32) sqp_lane_kernel<TwoLinkArm, float><<<grid, block, 0, stream>>>(p, lw);
+            else sqp_lane_kernel<TwoLinkArm, double><<<grid, block, 0, stream>>>(p, lw);
+        }
     }
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
@@ -455,7 +464,7 @@ void mmpc_default_opts(mmpc_opts* o) {
     o->tol_grad = 1e-8;
     o->tol_defect = 1e-10;
     o->kkt_solver = MMPC_KKT_AUTO;
-    o->reserved = 0;
+    o->factor_fp32 = 0;
 }
 
 int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_handle** out) {

@@ -21,6 +21,7 @@
 // Per-lane state lives in a structure-of-arrays workspace in HBM ([wave block][element][lane]), so every
 // wave access is one contiguous 512-byte line.
 #pragma once
+#include <limits>
 #include "models.h"
 #include "sqp_wave.h"
 
@@ -43,7 +44,7 @@ struct StageFields {
     static constexpr int D = C + NX;        // d_k (defect propagation)
     static constexpr int DX = D + NX;       // dx_k
     static constexpr int DU = DX + NX;      // du_k
-    static constexpr int K = DU + NU;       // [K_k | kff_k], nu x (nx+nu+1)
+    static constexpr int K = DU + NU;       // kff_k (nu, fp64) then K_k (nu x (nx+nu), factor type)
     static constexpr int SS = K + NU * (NS + 1);
     static_assert(SS == lane_stage_stride(NX, NU), "layout");
     static_assert(NX * NX <= SS, "Riccati scratch W fits one stage");
@@ -61,11 +62,11 @@ __host__ __device__ constexpr int sym_idx(int n, int i, int j) {
 // Products with the discrete stage matrices of a second-order model (x = [q; qd], xdot = [qd; acc]):
 //   A = I + h f_x = [[I, h I], [hFq, I + hFqd]],   B = h f_u = [[0], [hFu]]
 // where hFq = h dacc/dq, hFqd = h dacc/dqd, hFu = h dacc/du (row-major NQ x NQ / NQ x NU).
-template <int NQ>
-MMPC_HD void a_mul(double h, const double* hFq, const double* hFqd, const double* v, double* out) {
+template <int NQ, class T>
+MMPC_HD void a_mul(T h, const T* hFq, const T* hFqd, const T* v, T* out) {
 #pragma unroll
     for (int i = 0; i < NQ; ++i) {
-        double t = v[NQ + i];
+        T t = v[NQ + i];
 #pragma unroll
         for (int s = 0; s < NQ; ++s) t = fma(hFq[i * NQ + s], v[s], fma(hFqd[i * NQ + s], v[NQ + s], t));
         out[NQ + i] = t;
@@ -73,11 +74,11 @@ MMPC_HD void a_mul(double h, const double* hFq, const double* hFqd, const double
 #pragma unroll
     for (int i = 0; i < NQ; ++i) out[i] = fma(h, v[NQ + i], v[i]);
 }
-template <int NQ>
-MMPC_HD void at_mul(double h, const double* hFq, const double* hFqd, const double* v, double* out) {
+template <int NQ, class T>
+MMPC_HD void at_mul(T h, const T* hFq, const T* hFqd, const T* v, T* out) {
 #pragma unroll
     for (int a = 0; a < NQ; ++a) {
-        double tq = v[a], td = fma(h, v[a], v[NQ + a]);
+        T tq = v[a], td = fma(h, v[a], v[NQ + a]);
 #pragma unroll
         for (int s = 0; s < NQ; ++s) {
             tq = fma(hFq[s * NQ + a], v[NQ + s], tq);
@@ -97,7 +98,10 @@ __device__ __forceinline__ double* stage_ptr(double* wsb, int64_t k, int SS, int
     return q;
 }
 
-template <class Model>
+// FT: arithmetic type of the Riccati factor/solve (double, or float for SURVEY.md 8d cfg#5: the backward
+// recursion, P in LDS, the gains K and the W scratch in fp32; model evaluations, defects, adjoint, gradient,
+// merit and iterates stay fp64, so every SQP iteration refines the fp32 step against fp64 residuals).
+template <class Model, class FT = double>
 __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw) {
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NS = NX + NU, ND = NX + NU;
     static_assert(NX == 2 * NQ, "second-order models only (x = [q; qd])");
@@ -106,9 +110,9 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     MMPC_PHASE_DECL
     // Riccati matrix P~ (packed upper, NS(NS+1)/2 doubles per lane) lives in LDS, lane-interleaved
     // (conflict-free): holding it in registers next to the stage blocks and the factor spills to scratch.
-    __shared__ double sP[NS * (NS + 1) / 2][64];
+    __shared__ FT sP[NS * (NS + 1) / 2][64];
     if (inst >= p.B) return;  // lanes never exchange data
-    double* __restrict__ Pl = &sP[0][threadIdx.x];
+    FT* __restrict__ Pl = &sP[0][threadIdx.x];
 #define PS(i, j) Pl[sym_idx(NS, (i), (j)) * 64]
     const int N = p.N;
     const int NV = NX * (N + 1) + NU * N;
@@ -293,7 +297,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             for (int a = 0; a < NS; ++a) {
                 pv[a] = 0.0;
 #pragma unroll
-                for (int b = a; b < NS; ++b) PS(a, b) = (a == b && a < NX) ? Q[a] : 0.0;
+                for (int b = a; b < NS; ++b) PS(a, b) = (FT)((a == b && a < NX) ? Q[a] : 0.0);
             }
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -365,128 +369,157 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     }
                 }
                 // ---- Riccati step ----
-                double G[NX][NU];  // P_xx B + P_xu   (B = [0; hFu])
+                // Matrix recursion (P, G, H_ww, its Cholesky factor, the matrix part of Y and K) in FT; the
+                // right-hand side (p, m = P_xx c + p_x, h_w, y, kff) in fp64 with FT matrices: with FT = float
+                // this is an fp32 factorisation applied to fp64 residuals, so each SQP iteration is a
+                // refinement step (the linear terms cancel down to the gradient and need fp64).
+                FT fq[NQ * NQ], fqd[NQ * NQ], fu[NQ * NU];
+                const FT hf = (FT)h;
+#pragma unroll
+                for (int i = 0; i < NQ * NQ; ++i) {
+                    fq[i] = (FT)hFq[i];
+                    fqd[i] = (FT)hFqd[i];
+                }
+#pragma unroll
+                for (int i = 0; i < NQ * NU; ++i) fu[i] = (FT)hFu[i];
+                FT G[NX][NU];  // P_xx B + P_xu   (B = [0; hFu])
 #pragma unroll
                 for (int r = 0; r < NX; ++r)
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
-                        double t = PS(r, NX + c);
+                        FT t = PS(r, NX + c);
 #pragma unroll
-                        for (int s = 0; s < NQ; ++s) t = fma(PS(r, NQ + s), hFu[s * NU + c], t);
+                        for (int s = 0; s < NQ; ++s) t = fma(PS(r, NQ + s), fu[s * NU + c], t);
                         G[r][c] = t;
                     }
-                double mv[NX];  // P_xx c + p_x
+                double mv[NX];  // P_xx c + p_x (fp64)
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
                     double t = pv[r];
 #pragma unroll
-                    for (int q = 0; q < NX; ++q) t = fma(PS(r, q), cc[q], t);
+                    for (int q = 0; q < NX; ++q) t = fma((double)PS(r, q), cc[q], t);
                     mv[r] = t;
                 }
-                double Hww[NU][NU], Y[NU][NS + 1];  // Y rows: L^-1 [H_wx | -R | h_w]
+                FT Hww[NU][NU], Y[NU][NS];  // Y rows: L^-1 [H_wx | -R]
+                double yh[NU];              // L^-1 h_w (fp64)
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
 #pragma unroll
                     for (int b = a; b < NU; ++b) {
-                        double t = PS(NX + a, NX + b);
+                        FT t = PS(NX + a, NX + b);
 #pragma unroll
                         for (int s = 0; s < NQ; ++s)
-                            t = fma(hFu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), hFu[s * NU + b], t));
-                        if (a == b) t += R[a] + Rm[a];
+                            t = fma(fu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), fu[s * NU + b], t));
+                        if (a == b) t += (FT)(R[a] + Rm[a]);
                         Hww[a][b] = t;
                     }
                     double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
 #pragma unroll
                     for (int s = 0; s < NQ; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) t = fma(PS(r, NX + a), cc[r], t);
-                    Y[a][NS] = t;
-                    double ga[NX];
+                    for (int r = 0; r < NX; ++r) t = fma((double)PS(r, NX + a), cc[r], t);
+                    yh[a] = t;
+                    FT ga[NX];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) ga[r] = G[r][a];
-                    at_mul<NQ>(h, hFq, hFqd, ga, &Y[a][0]);  // H_wx row a = (A^T G[:, a])^T
+                    at_mul<NQ, FT>(hf, fq, fqd, ga, &Y[a][0]);  // H_wx row a = (A^T G[:, a])^T
 #pragma unroll
-                    for (int c = 0; c < NU; ++c) Y[a][NX + c] = (a == c) ? -R[a] : 0.0;
+                    for (int c = 0; c < NU; ++c) Y[a][NX + c] = (FT)((a == c) ? -R[a] : 0.0);
                 }
                 // W = P_xx A (row r of W = (A^T P_xx[r][:])^T), streamed through the lane's scratch stage of the
-                // workspace: held in registers next to G, Y and the stage blocks it spills (1.2 KB/lane).
-                // p~_k x part: A^T mv + Q (x_k - r_{k-1}).
+                // workspace (in registers next to G, Y and the stage blocks it spills).
+                // p~_k x part: A^T mv + Q (x_k - r_{k-1}) (fp64).
                 double pn[NS];
-                double* const sw = stage_ptr(wsb, N + 2, SS, lane);  // per-lane scratch stage
+                FT* const sw = reinterpret_cast<FT*>(stage_ptr(wsb, N + 2, SS, 0)) + lane;  // per-lane scratch stage
                 if (k >= 1) {
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
-                        double prow[NX], wrow[NX];
+                        FT prow[NX], wrow[NX];
 #pragma unroll
                         for (int q = 0; q < NX; ++q) prow[q] = PS(r, q);
-                        at_mul<NQ>(h, hFq, hFqd, prow, wrow);
+                        at_mul<NQ, FT>(hf, fq, fqd, prow, wrow);
 #pragma unroll
                         for (int b = 0; b < NX; ++b) sw[(r * NX + b) * 64] = wrow[b];
                     }
                     double t[NX];
-                    at_mul<NQ>(h, hFq, hFqd, mv, t);
+                    at_mul<NQ, double>(h, hFq, hFqd, mv, t);
 #pragma unroll
                     for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - rkm[q], t[q]);
 #pragma unroll
                     for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
                 }
-                // Cholesky H_ww = L L^T, then Y <- L^-1 Y
-                double Ld[NU][NU], il[NU];
+                // Cholesky H_ww = L L^T (FT), then Y <- L^-1 Y (FT) and yh <- L^-1 yh (fp64)
+                FT Ld[NU][NU], il[NU];
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
-                    double s = Hww[a][a];
+                    FT s = Hww[a][a];
 #pragma unroll
                     for (int q = 0; q < a; ++q) s = fma(-Ld[a][q], Ld[a][q], s);
-                    fact_ok &= (s > 0.0) && isfinite(s);
-                    const double lj = sqrt(fmax(s, 1e-300));
+                    fact_ok &= (s > (FT)0) && isfinite(s);
+                    const FT lj = sqrt(fmax(s, std::numeric_limits<FT>::min()));
                     Ld[a][a] = lj;
-                    il[a] = 1.0 / lj;
+                    il[a] = (FT)1 / lj;
 #pragma unroll
                     for (int b = a + 1; b < NU; ++b) {
-                        double t = Hww[a][b];
+                        FT t = Hww[a][b];
 #pragma unroll
                         for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
                         Ld[b][a] = t * il[a];
                     }
                 }
 #pragma unroll
-                for (int a = 0; a < NU; ++a)
+                for (int a = 0; a < NU; ++a) {
 #pragma unroll
-                    for (int j = 0; j <= NS; ++j) {
-                        double t = Y[a][j];
+                    for (int j = 0; j < NS; ++j) {
+                        FT t = Y[a][j];
 #pragma unroll
                         for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
                         Y[a][j] = t * il[a];
                     }
-                // [K_k | kff_k] = -L^-T Y
+                    double t = yh[a];
+#pragma unroll
+                    for (int q = 0; q < a; ++q) t = fma(-(double)Ld[a][q], yh[q], t);
+                    yh[a] = t / (double)Ld[a][a];
+                }
+                // [K_k | kff_k] = -L^-T [Y | yh]: kff (fp64) in the first NU slots of the K field, K (FT) after it
                 {
-                    double Kt[NU][NS + 1];
+                    FT Kt[NU][NS];
+                    double kh[NU];
 #pragma unroll
-                    for (int a = NU - 1; a >= 0; --a)
+                    for (int a = NU - 1; a >= 0; --a) {
 #pragma unroll
-                        for (int j = 0; j <= NS; ++j) {
-                            double t = Y[a][j];
+                        for (int j = 0; j < NS; ++j) {
+                            FT t = Y[a][j];
 #pragma unroll
                             for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], Kt[q][j], t);
                             Kt[a][j] = t * il[a];
                         }
+                        double t = yh[a];
 #pragma unroll
-                    for (int a = 0; a < NU; ++a)
+                        for (int q = a + 1; q < NU; ++q) t = fma(-(double)Ld[q][a], kh[q], t);
+                        kh[a] = t / (double)Ld[a][a];
+                    }
+                    double* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
+                    FT* const kk = reinterpret_cast<FT*>(kb + NU * 64) + lane;
 #pragma unroll
-                        for (int j = 0; j <= NS; ++j) SK(0, SF::K, a * (NS + 1) + j) = -Kt[a][j];
+                    for (int a = 0; a < NU; ++a) {
+                        kb[a * 64 + lane] = -kh[a];
+#pragma unroll
+                        for (int j = 0; j < NS; ++j) kk[(a * NS + j) * 64] = -Kt[a][j];
+                    }
                 }
                 if (k == 0) break;  // s_0 = 0: P~_0 is never used
-                // P~_k = blkdiag(A^T W + Q, R) - Y^T Y (old P is dead: overwrite it in place), p~_k = pn - Y^T y
+                // P~_k = blkdiag(A^T W + Q, R) - Y^T Y (old P is dead: overwrite it in place), p~_k = pn - Y^T yh
                 asm volatile("" ::: "memory");  // W comes back from memory, not from forwarded registers
 #pragma unroll
                 for (int b = 0; b < NX; ++b) {
-                    double wcol[NX], col[NX];
+                    FT wcol[NX], col[NX];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) wcol[r] = sw[(r * NX + b) * 64];
-                    at_mul<NQ>(h, hFq, hFqd, wcol, col);
+                    at_mul<NQ, FT>(hf, fq, fqd, wcol, col);
 #pragma unroll
                     for (int a = 0; a <= b; ++a) {
-                        double v = col[a] + ((a == b) ? Q[a] : 0.0);
+                        FT v = col[a] + (FT)((a == b) ? Q[a] : 0.0);
 #pragma unroll
                         for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
                         PS(a, b) = v;
@@ -496,11 +529,11 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 for (int a = 0; a < NS; ++a) {
                     double t = pn[a];
 #pragma unroll
-                    for (int q = 0; q < NU; ++q) t = fma(-Y[q][a], Y[q][NS], t);
+                    for (int q = 0; q < NU; ++q) t = fma(-(double)Y[q][a], yh[q], t);
                     pv[a] = t;
 #pragma unroll
                     for (int b = (a < NX ? NX : a); b < NS; ++b) {
-                        double v = (a == b) ? R[a - NX] : 0.0;
+                        FT v = (FT)((a == b) ? R[a - NX] : 0.0);
 #pragma unroll
                         for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
                         PS(a, b) = v;
@@ -574,14 +607,16 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     upf[c] = SK(1, SF::U, c);  // stage N's U slot exists (unused) when k = N-1
                 }
                 double du[NU];
+                const double* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
+                const FT* const kk = reinterpret_cast<const FT*>(kb + NU * 64) + lane;
 #pragma unroll
                 for (int a = 0; a < NU; ++a) {
-                    const int base = a * (NS + 1);
-                    double t = SK(0, SF::K, base + NS);
+                    const int base = a * NS;
+                    double t = kb[a * 64 + lane];
 #pragma unroll
-                    for (int q = 0; q < NX; ++q) t = fma(SK(0, SF::K, base + q), dx[q], t);
+                    for (int q = 0; q < NX; ++q) t = fma((double)kk[(base + q) * 64], dx[q], t);
 #pragma unroll
-                    for (int c = 0; c < NU; ++c) t = fma(SK(0, SF::K, base + NX + c), dup[c], t);
+                    for (int c = 0; c < NU; ++c) t = fma((double)kk[(base + NX + c) * 64], dup[c], t);
                     du[a] = t;
                     SK(0, SF::DU, a) = t;
                 }

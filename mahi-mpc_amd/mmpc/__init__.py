@@ -45,7 +45,7 @@ MODEL_TWO_LINK_ARM, MODEL_EXO_ARM = 0, 1
 
 class Opts(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("device", C.c_int32), ("tol_grad", C.c_double),
-                ("tol_defect", C.c_double), ("kkt_solver", C.c_int32), ("reserved", C.c_int32)]
+                ("tol_defect", C.c_double), ("kkt_solver", C.c_int32), ("factor_fp32", C.c_int32)]
 
 
 class ModelInfo(C.Structure):
@@ -159,10 +159,12 @@ class Solver:
     """One loaded model (the reference's ModelControl without the thread/bookkeeping)."""
 
     def __init__(self, model_json=None, json_text=None, max_iter=None, tol_grad=None, tol_defect=None,
-                 device=None, kkt_solver=None):
+                 device=None, kkt_solver=None, factor_fp32=None):
         o = default_opts()
         if kkt_solver is not None:
             o.kkt_solver = kkt_solver
+        if factor_fp32 is not None:
+            o.factor_fp32 = int(factor_fp32)
         if max_iter is not None:
             o.max_iter = max_iter
         if tol_grad is not None:

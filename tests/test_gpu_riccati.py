@@ -228,3 +228,29 @@ def test_riccati_weights_bounds_nonfinite_warmstart(exo_solver, oracle):
     o5 = oracle.solve_batch(N, H, x0[:4], up[:4], tr[:4], W_EXO, max_iter=1, model=oracle.EXO)
     assert (r5["status"] == 1).all() and (r5["iters"] == 1).all()
     assert _rel(r5["V"], o5["V"]).max() < 1e-9
+
+
+def test_fp32_factor_converges_to_the_fp64_solution(exo_solver, model_json, mmpc_mod, oracle):
+    """SURVEY.md 8d cfg#5: fp32 Riccati factor, fp64 residuals.  Same KKT point to the accuracy the stop test
+    guarantees (1e-6 relative in V*), every instance converged; the fp64 residual test is unchanged."""
+    N = 50
+    x0, up, tr = oracle.synth(20250213, 0, 256, N, H, model=oracle.EXO)
+    r32 = exo_solver(factor_fp32=1).solve_batch_host(x0, up, tr, W_EXO)
+    o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, model=oracle.EXO)
+    assert (r32["status"] == 0).all(), np.bincount(r32["status"])
+    assert (r32["kkt"] <= 1e-8).all()
+    assert _rel(r32["V"], o["V"]).max() <= 1e-6
+    x0, up, tr = oracle.synth(5, 0, 128, 30, H)
+    w = np.array(WEIGHTS_CFG)
+    r32 = mmpc_mod.Solver(model_json(N=30), factor_fp32=1).solve_batch_host(x0, up, tr, w)
+    o = oracle.solve_batch(30, H, x0, up, tr, w)
+    assert (r32["status"] == 0).all()
+    assert _rel(r32["V"], o["V"]).max() <= 1e-6
+
+
+def test_fp32_factor_is_riccati_only(model_json, mmpc_mod, oracle):
+    x0, up, tr = oracle.synth(5, 0, 2, 30, H)
+    s = mmpc_mod.Solver(model_json(N=30), factor_fp32=1, kkt_solver=mmpc_mod.KKT_CONDENSED)
+    with pytest.raises(mmpc_mod.MmpcError) as ei:
+        s.solve_batch_host(x0, up, tr, np.array(WEIGHTS_CFG))
+    assert ei.value.code == -4
