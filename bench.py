@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
                     help="cfg2 = headline (BASELINE.json); cfg3 = exo workload of SURVEY.md 8d")
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU (cfg#2: 4096, cfg#3: 65536)")
+    ap.add_argument("--kkt", choices=["auto", "condensed", "riccati", "group"], default="auto",
+                    help="KKT solver (mmpc_opts.kkt_solver); auto = the library's choice")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -108,9 +110,12 @@ def main():
     tmpdir = tempfile.mkdtemp(prefix="mmpc_bench_")
     path = mmpc.write_model_json(os.path.join(tmpdir, f"{cfg['model']}.json"), cfg["model"], nx, nu, h_us, N,
                                  model=cfg["model"])
-    solver = mmpc.Solver(path, device=local)
+    ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt]
+    solver = mmpc.Solver(path, device=local, kkt_solver=ksolver)
     solver.reserve_workspace(B)
-    riccati = cfg["model"] != "two_link_arm" or N * nu > 64
+    if ksolver == 0:
+        ksolver = 1 if (cfg["model"] == "two_link_arm" and N * nu <= 64) else 2
+    riccati = ksolver in (2, 3)
     NV = solver.NV
     f64 = dict(dtype=torch.float64, device=dev)
     x0 = torch.empty((B, nx), **f64)
@@ -163,7 +168,8 @@ def main():
         fl = mmpc.riccati_flops_per_iteration(N, nx, nu)
         own_fl = float(iters.sum()) * fl["total"]
         achieved = own_fl / (kern_ms * 1e-3) / 1e12
-        kname = f"sqp_lane_kernel<{'ExoArm' if cfg['model'] == 'exo_arm' else 'TwoLinkArm'}>"
+        kname = (f"sqp_{'group' if ksolver == 3 else 'lane'}_kernel<"
+                 f"{'ExoArm' if cfg['model'] == 'exo_arm' else 'TwoLinkArm'}>")
     else:
         fl = mmpc.flops_per_iteration(N)
         own_fl = float(iters.sum()) * fl["total"]
@@ -191,7 +197,8 @@ def main():
         "dtype": "f64",
         "data": f"synthetic: counter-based splitmix64 {args.config} instances (SURVEY.md 8d), generated on device",
         "config": {"workload": cfg["workload"], "batch_per_gpu": B, "global_batch": B * world,
-                   "horizon": N, "kkt_solver": "riccati (lane per instance)" if riccati else "condensed (wave per instance)",
+                   "horizon": N, "kkt_solver": {1: "condensed (wave per instance)", 2: "riccati (lane per instance)",
+                                                3: "riccati (16 lanes per instance)"}[ksolver],
                    "parallelism": f"batch-shard x{world} (no data-path collective)"},
         "converged": conv,
         "mean_sqp_iters": float(iters.mean()),

@@ -93,9 +93,12 @@ enum mmpc_model_id {
 
 /* KKT solve of each SQP iteration (both solve the same Gauss-Newton QP exactly) */
 enum mmpc_kkt_solver {
-    MMPC_KKT_AUTO = 0,      /* condensed when N*nu <= 64 and the model is the 2-link arm, else Riccati */
+    MMPC_KKT_AUTO = 0,      /* 2-link arm: condensed when N*nu <= 64, else the 16-lane Riccati solver for
+                               B <= 8192 when its LDS fits; otherwise one lane per instance */
     MMPC_KKT_CONDENSED = 1, /* one wavefront per instance, condensed Hessian row per lane (N*nu <= 64) */
-    MMPC_KKT_RICCATI = 2    /* one lane per instance, Riccati recursion, any N (needs a workspace) */
+    MMPC_KKT_RICCATI = 2,   /* one lane per instance, Riccati recursion, any N (needs a workspace) */
+    MMPC_KKT_RICCATI_GROUP = 3 /* 16 lanes per instance: stage-parallel model evaluations and line search,
+                                  serial Riccati sweeps from LDS (stage data of 4 instances <= 160 KB LDS) */
 };
 
 typedef struct mmpc_opts {
@@ -131,8 +134,8 @@ int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_han
 int mmpc_destroy(mmpc_handle* h);
 int mmpc_get_model_info(const mmpc_handle* h, mmpc_model_info* info);
 int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts);
-/* Pre-allocate the Riccati solver's device workspace for batches up to B (no-op for the
- * condensed solver).  *bytes (may be NULL) receives the workspace size. */
+/* Pre-allocate the Riccati solvers' device workspace for batches up to B (so that later
+ * stream-ordered solves allocate nothing; the workspace grows on demand otherwise).  *bytes (may be NULL) receives the workspace size. */
 int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes);
 
 /* Batched SQP solve, DEVICE pointers, stream-ordered.  u_lb/u_ub: device [nu] or NULL

@@ -6,6 +6,7 @@
 // exists: every compute entry point runs on the GPU or returns an error.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdio>
@@ -19,6 +20,7 @@
 #include "../../include/mmpc.h"
 #include "json_lite.h"
 #include "models.h"
+#include "sqp_group.h"
 #include "sqp_lane.h"
 #include "sqp_wave.h"
 
@@ -165,7 +167,7 @@ int parse_model(const std::string& text, mmpc_model_info* info) {
 int validate_opts(const mmpc_opts* o) {
     if (o->max_iter < 0 || o->max_iter > 100000) return fail(MMPC_ERR_INVALID_ARG, "max_iter out of range");
     if (!(o->tol_grad > 0.0) || !(o->tol_defect > 0.0)) return fail(MMPC_ERR_INVALID_ARG, "tolerances must be > 0");
-    if (o->kkt_solver < MMPC_KKT_AUTO || o->kkt_solver > MMPC_KKT_RICCATI)
+    if (o->kkt_solver < MMPC_KKT_AUTO || o->kkt_solver > MMPC_KKT_RICCATI_GROUP)
         return fail(MMPC_ERR_INVALID_ARG, "unknown kkt_solver");
     if (o->factor_fp32 != 0 && o->factor_fp32 != 1) return fail(MMPC_ERR_INVALID_ARG, "factor_fp32 must be 0 or 1");
     return MMPC_OK;
@@ -349,10 +351,27 @@ size_t workspace_bytes(const mmpc_model_info& mi, int64_t B) {
            static_cast<size_t>(blocks) * sizeof(double);
 }
 
-// Riccati workspace for B instances (SoA per 64-instance block, sqp_lane.h).  Growth is synchronous:
+size_t group_workspace_bytes(const mmpc_model_info& mi, int64_t B) {
+    return static_cast<size_t>(group_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) *
+           static_cast<size_t>(B) * sizeof(double);
+}
+size_t group_lds_bytes(const mmpc_model_info& mi) {
+    return static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) * kGroupsPerWave *
+           sizeof(double);
+}
+constexpr size_t kMaxGroupLds = 160 * 1024;  // gfx950: 160 KB of LDS per workgroup (attribute raised above 64 KB)
+
+template <class K>
+int set_dynamic_lds(K kernel, size_t bytes) {
+    if (bytes <= 64 * 1024) return MMPC_OK;
+    MMPC_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 static_cast<int>(bytes)));
+    return MMPC_OK;
+}
+
+// Riccati workspace (sqp_lane.h / sqp_group.h layouts), grown on demand.  Growth is synchronous:
 // hipFree waits for the kernels still using the old buffer.
-int ensure_workspace(mmpc_handle* h, int64_t B, LaneWork* lw) {
-    const size_t bytes = workspace_bytes(h->info, B);
+int ensure_workspace_bytes(mmpc_handle* h, size_t bytes, double** out) {
     int dev = -1;
     MMPC_HIP(hipGetDevice(&dev));
     std::lock_guard<std::mutex> lk(h->ws_mu);
@@ -365,8 +384,11 @@ int ensure_workspace(mmpc_handle* h, int64_t B, LaneWork* lw) {
         h->ws_bytes = bytes;
         h->ws_dev = dev;
     }
-    lw->ws = h->ws;
+    *out = h->ws;
     return MMPC_OK;
+}
+int ensure_workspace(mmpc_handle* h, int64_t B, LaneWork* lw) {
+    return ensure_workspace_bytes(h, std::max(workspace_bytes(h->info, B), group_workspace_bytes(h->info, B)), &lw->ws);
 }
 
 int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
@@ -402,8 +424,35 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     const int N = mi.num_shooting_nodes;
     int solver = h->opts.kkt_solver;
     const bool condensed_ok = mi.model_id == MMPC_MODEL_TWO_LINK_ARM && N * TwoLinkArm::NU <= 64;
-    if (solver == MMPC_KKT_AUTO)
-        solver = (condensed_ok && !h->opts.factor_fp32) ? MMPC_KKT_CONDENSED : MMPC_KKT_RICCATI;
+    if (solver == MMPC_KKT_AUTO) {
+        // measured on one MI355X: condensed when it fits; for the 2-link arm 16 lanes per instance
+        // while one lane per instance would leave most SIMDs idle (B <= 8192); otherwise one lane per instance
+        // (the exo model's 12x12 serial recursion is faster lane-per-instance even at B = 4096)
+        if (condensed_ok && !h->opts.factor_fp32) solver = MMPC_KKT_CONDENSED;
+        else if (!h->opts.factor_fp32 && mi.model_id == MMPC_MODEL_TWO_LINK_ARM && B <= 8192 &&
+                 group_lds_bytes(mi) <= kMaxGroupLds)
+            solver = MMPC_KKT_RICCATI_GROUP;
+        else solver = MMPC_KKT_RICCATI;
+    }
+    if (solver == MMPC_KKT_RICCATI_GROUP) {
+        if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 needs the lane Riccati solver");
+        const size_t lds = group_lds_bytes(mi);
+        if (lds > kMaxGroupLds) return fail(MMPC_ERR_UNSUPPORTED, "group Riccati solver: stage data exceeds 160 KB LDS");
+        LaneWork lw;
+        int rc = ensure_workspace(h, B, &lw);
+        if (rc) return rc;
+        GroupWork gwk{lw.ws};
+        dim3 grid(grid1d(B, kGroupsPerWave)), block(64);
+        if (mi.model_id == MMPC_MODEL_EXO_ARM) {
+            if ((rc = set_dynamic_lds(sqp_group_kernel<ExoArm>, lds))) return rc;
+            sqp_group_kernel<ExoArm><<<grid, block, lds, stream>>>(p, gwk);
+        } else {
+            if ((rc = set_dynamic_lds(sqp_group_kernel<TwoLinkArm>, lds))) return rc;
+            sqp_group_kernel<TwoLinkArm><<<grid, block, lds, stream>>>(p, gwk);
+        }
+        MMPC_HIP(hipGetLastError());
+        return MMPC_OK;
+    }
     if (solver == MMPC_KKT_CONDENSED) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 is a Riccati-solver option");
         // host-side shape checks: the kernel holds one condensed-Hessian row per lane

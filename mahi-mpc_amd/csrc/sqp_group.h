@@ -1,0 +1,644 @@
+// sqp_group.h -- batched GN-SQP with a Riccati KKT solve, SIXTEEN LANES PER INSTANCE (four instances per wave).
+//
+// The condensed kernel (sqp_wave.h) spends O(N^2 nu^2 nx + (N nu)^3) flops per SQP iteration (288 kflop at
+// cfg#2); a Riccati recursion solves the same GN QP exactly in O(N (nx+nu)^3) (~15 kflop at
+// cfg#2).  The lane-per-instance Riccati kernel (sqp_lane.h) cannot fill the GPU at cfg#2's B = 4096 (64 waves),
+// so here one instance owns a 16-lane DPP row and the work splits by its shape:
+//   * stage-parallel (all 16 lanes, stage k on lane k mod 16): model + Jacobian evaluations, defects, merit
+//     terms, line-search trial evaluations, iterate updates, loads and stores;
+//   * O(N) recursions (one lane per instance): defect propagation d, adjoint + reduced gradient + Riccati
+//     backward sweep, forward step sweep -- reading the stage blocks the other lanes left in LDS.
+// Group reductions (J, |c|_1, max|c|, merit) are 16-lane butterflies; the NLP, merit, line search and stop test
+// are those of sqp_wave.h / sqp_lane.h / oracle.  B = 4096 gives 1024 waves = one per SIMD.
+//
+// LDS per instance (fp64): x_k, u_k, F_k, c_k, hFq_k, hFqd_k, hFu_k, d_k, dx_k, du_k (cross-lane data); the
+// targets stay in HBM (read-only) and the gains K_k in a per-instance HBM workspace (serial lane only).
+#pragma once
+#include "models.h"
+#include "sqp_lane.h"
+#include "sqp_wave.h"
+
+namespace mmpc {
+
+constexpr int kGroupLanes = 16;
+constexpr int kGroupsPerWave = 4;
+
+// LDS doubles per instance
+__host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int N) {
+    return N * (3 * nx + 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + nu + nu) + 3 * (N + 1) * nx;
+}
+// HBM workspace doubles per instance: K_k | kff_k per stage
+__host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) { return N * nu * (nx + nu + 1); }
+
+struct GroupWork {
+    double* ws;
+};
+
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double group_max(double v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double group_bcast(double v, int base) { return __shfl(v, base); }
+__device__ __forceinline__ int group_bcast_i(int v, int base) { return __shfl(v, base); }
+
+// xd = f(x, u); with jac also the acceleration partials (unscaled).  Linear mode (ModelGenerator.cpp:47-48):
+// F_lin with the acceleration Jacobians lFq, lFqd, lFu and xdot lxd taken at (lxs, lus).
+template <class Model>
+__device__ __forceinline__ void group_model(bool lin, const double* lFq, const double* lFqd, const double* lFu,
+                                            const double* lxd, const double* lxs, const double* lus, const double* x,
+                                            const double* u, double* xd, double* Fq, double* Fqd, double* Fu,
+                                            bool jac) {
+    constexpr int NQ = Model::NQ, NU = Model::NU;
+    if (!lin) {
+        if (jac) {
+            Model::eval_acc_jac(x, u, xd + NQ, Fq, Fqd, Fu);
+#pragma unroll
+            for (int i = 0; i < NQ; ++i) xd[i] = x[NQ + i];
+        } else {
+            Model::eval(x, u, xd);
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) {
+        xd[i] = lxd[i] + (x[NQ + i] - lxs[NQ + i]);
+        double t = lxd[NQ + i];
+#pragma unroll
+        for (int s = 0; s < NQ; ++s)
+            t = fma(lFq[i * NQ + s], x[s] - lxs[s], fma(lFqd[i * NQ + s], x[NQ + s] - lxs[NQ + s], t));
+#pragma unroll
+        for (int c = 0; c < NU; ++c) t = fma(lFu[i * NU + c], u[c] - lus[c], t);
+        xd[NQ + i] = t;
+    }
+    if (jac) {
+#pragma unroll
+        for (int i = 0; i < NQ * NQ; ++i) {
+            Fq[i] = lFq[i];
+            Fqd[i] = lFqd[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NQ * NU; ++i) Fu[i] = lFu[i];
+    }
+}
+
+template <class Model>
+__global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork gw) {
+    constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NS = NX + NU, ND = NX + NU;
+    constexpr int G = kGroupLanes;
+    extern __shared__ double shm[];
+    const int gl = threadIdx.x & (G - 1);
+    const int gi = threadIdx.x / G;
+    [[maybe_unused]] const int lane0 = threadIdx.x;
+    MMPC_PHASE_DECL
+    const int gbase = gi * G;  // first lane of this instance's group
+    const int64_t inst = (int64_t)blockIdx.x * kGroupsPerWave + gi;
+    const bool valid = inst < p.B;
+    const int64_t ii = valid ? inst : 0;  // invalid groups are masked by `done` and touch instance 0 read-only
+    const int N = p.N;
+    const int NV = NX * (N + 1) + NU * N;
+    const double h = p.h;
+
+    // ---- LDS views of this instance ----
+    double* const sX = shm + gi * group_lds_doubles(NX, NU, N);  // [N+1][NX]
+    double* const sDX = sX + (N + 1) * NX;                         // [N+1][NX]
+    double* const sD = sDX + (N + 1) * NX;                         // [N+1][NX]
+    double* const sU = sD + (N + 1) * NX;                          // [N][NU]
+    double* const sDU = sU + N * NU;                               // [N][NU]
+    double* const sF = sDU + N * NU;                               // [N][NX]
+    double* const sC = sF + N * NX;                                // [N][NX]
+    double* const sFq = sC + N * NX;                               // [N][NQ*NQ]   h dacc/dq
+    double* const sFqd = sFq + N * NQ * NQ;                        // [N][NQ*NQ]   h dacc/dqd
+    double* const sFu = sFqd + N * NQ * NQ;                        // [N][NQ*NU]   h dacc/du
+    double* const sR = sFu + N * NQ * NU;                          // [N][NX]      targets r_k
+    double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
+    const double* const trg = p.traj + ii * (int64_t)N * NX;
+
+    const double* w = p.weights + ii * p.w_stride;
+    double Q[NX], R[NU], Rm[NU], up[NU];
+#pragma unroll
+    for (int r = 0; r < NX; ++r) Q[r] = w[r];
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        R[c] = w[NX + c];
+        Rm[c] = w[NX + NU + c];
+        up[c] = p.u_prev[ii * NU + c];
+    }
+    // ---- load: V (reference layout) -> LDS, x_0 pinned (ModelControl.cpp:144-145) ----
+    {
+        const double* Vin = p.V + ii * (int64_t)NV;
+        for (int k = gl; k <= N; k += G) {
+#pragma unroll
+            for (int r = 0; r < NX; ++r) sX[k * NX + r] = (k == 0) ? p.x0[ii * NX + r] : Vin[k * ND + r];
+            if (k < N) {
+#pragma unroll
+                for (int c = 0; c < NU; ++c) sU[k * NU + c] = Vin[k * ND + NX + c];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) sR[k * NX + r] = trg[k * NX + r];
+            }
+        }
+    }
+    const double* const tr = sR;
+    // linear mode: acceleration Jacobians and xdot at (x_0, u_prev) (ModelControl.cpp:125-135), in registers
+    const bool lin = p.is_linear != 0;
+    double lFq[NQ * NQ], lFqd[NQ * NQ], lFu[NQ * NU], lxd[NX], lxs[NX];
+    if (lin) {
+        double acc[NQ];
+#pragma unroll
+        for (int r = 0; r < NX; ++r) lxs[r] = p.x0[ii * NX + r];
+        Model::eval_acc_jac(lxs, up, acc, lFq, lFqd, lFu);
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) {
+            lxd[i] = lxs[NQ + i];
+            lxd[NQ + i] = acc[i];
+        }
+    }
+    int status = ST_MAX_ITER;
+    int it = 0;
+    double kkt = 0.0, mu = 0.0;
+    bool done = !valid;
+    MMPC_PHASE(0);
+    for (it = 0; !done; ++it) {
+        __builtin_amdgcn_wave_barrier();
+        // ---- A. stage-parallel: F_k, A_k/B_k blocks, defects, merit value ----
+        double J0 = 0.0, c1 = 0.0, cmax = 0.0;
+        int nonfinite = 0;
+        for (int k = gl; k < N; k += G) {
+            double x[NX], u[NU], xd[NX], Fq[NQ * NQ], Fqd[NQ * NQ], Fu[NQ * NU];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) x[r] = sX[k * NX + r];
+#pragma unroll
+            for (int c = 0; c < NU; ++c) u[c] = sU[k * NU + c];
+            group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, Fq, Fqd, Fu, true);
+#pragma unroll
+            for (int i = 0; i < NQ * NQ; ++i) {
+                sFq[k * NQ * NQ + i] = h * Fq[i];
+                sFqd[k * NQ * NQ + i] = h * Fqd[i];
+            }
+#pragma unroll
+            for (int i = 0; i < NQ * NU; ++i) sFu[k * NQ * NU + i] = h * Fu[i];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                const double F = fma(h, xd[r], x[r]);
+                sF[k * NX + r] = F;
+                const double c = F - sX[(k + 1) * NX + r];
+                sC[k * NX + r] = c;
+                cmax = fmax(cmax, fabs(c));
+                c1 += fabs(c);
+                nonfinite |= !isfinite(c);
+                const double e = F - tr[k * NX + r];
+                J0 = fma(e * Q[r], e, J0);
+            }
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                const double um = (k == 0) ? up[c] : sU[(k - 1) * NU + c];
+                const double dif = u[c] - um;
+                J0 = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], J0));
+            }
+        }
+        J0 = group_sum(J0);
+        c1 = group_sum(c1);
+        cmax = group_max(cmax);
+        __builtin_amdgcn_wave_barrier();
+        MMPC_PHASE(1);
+
+        // ---- B. one lane: d recursion, then adjoint + gradient + Riccati backward sweep (the 6x6 / 12x12
+        //      Riccati step of one stage is too small to pay for lane-parallel exchanges: measured slower) ----
+        double gmax = 0.0, lmax = 0.0;
+        int fact_ok = 1;
+        if (gl == 0) {
+            {
+                double d[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    d[r] = 0.0;
+                    sD[r] = 0.0;
+                }
+                for (int k = 0; k < N; ++k) {
+                    double dn[NX];
+                    a_mul<NQ, double>(h, sFq + k * NQ * NQ, sFqd + k * NQ * NQ, d, dn);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        d[r] = dn[r] + sC[k * NX + r];
+                        sD[(k + 1) * NX + r] = d[r];
+                    }
+                }
+            }
+            // P~ (symmetric, upper triangle used) and p~ on s = [dx_k; du_{k-1}]; P~_N = blkdiag(Q, 0)
+            double P[NS][NS], pv[NS], lam[NX], unext[NU];
+#define Ps(i, j) ((i) <= (j) ? P[(i)][(j)] : P[(j)][(i)])
+#pragma unroll
+            for (int a = 0; a < NS; ++a) {
+                pv[a] = 0.0;
+#pragma unroll
+                for (int b = a; b < NS; ++b) P[a][b] = (a == b && a < NX) ? Q[a] : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                const double eb = sX[N * NX + r] - tr[(N - 1) * NX + r];  // x_N - r_{N-1}
+                pv[r] = Q[r] * eb;
+                lam[r] = Q[r] * (sD[N * NX + r] + eb);  // lam_N = Q e_{N-1}
+                lmax = fmax(lmax, fabs(lam[r]));
+            }
+#pragma unroll
+            for (int c = 0; c < NU; ++c) unext[c] = 0.0;
+            for (int k = N - 1; k >= 0; --k) {
+                const double* hFq = sFq + k * NQ * NQ;
+                const double* hFqd = sFqd + k * NQ * NQ;
+                double hFu[NQ * NU], x[NX], u[NU], um[NU], cc[NX];
+#pragma unroll
+                for (int i = 0; i < NQ * NU; ++i) hFu[i] = sFu[k * NQ * NU + i];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    x[r] = sX[k * NX + r];
+                    cc[r] = sC[k * NX + r];
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    u[c] = sU[k * NU + c];
+                    um[c] = (k == 0) ? up[c] : sU[(k - 1) * NU + c];
+                }
+                // reduced gradient g_k = B_k^T lam_{k+1} + R/Rm terms
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    double g = 0.0;
+#pragma unroll
+                    for (int s = 0; s < NQ; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
+                    g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
+                    if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
+                    gmax = fmax(gmax, fabs(2.0 * g));
+                    nonfinite |= !isfinite(g);
+                    unext[c] = u[c];
+                }
+                // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1},  e_{k-1} = d_k + x_k - r_{k-1}
+                if (k >= 1) {
+                    double ln[NX];
+                    at_mul<NQ, double>(h, hFq, hFqd, lam, ln);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        lam[r] = fma(Q[r], sD[k * NX + r] + x[r] - tr[(k - 1) * NX + r], ln[r]);
+                        lmax = fmax(lmax, fabs(lam[r]));
+                    }
+                }
+                // Riccati step (sqp_lane.h): G = P_xx B + P_xu, H_ww, h_w, Y = L^-1 [H_wx | -R | h_w]
+                double Gm[NX][NU];
+#pragma unroll
+                for (int r = 0; r < NX; ++r)
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {
+                        double t = Ps(r, NX + c);
+#pragma unroll
+                        for (int s = 0; s < NQ; ++s) t = fma(Ps(r, NQ + s), hFu[s * NU + c], t);
+                        Gm[r][c] = t;
+                    }
+                double mv[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    double t = pv[r];
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) t = fma(Ps(r, q), cc[q], t);
+                    mv[r] = t;
+                }
+                double Hww[NU][NU], Y[NU][NS + 1];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+#pragma unroll
+                    for (int b = a; b < NU; ++b) {
+                        double t = Ps(NX + a, NX + b);
+#pragma unroll
+                        for (int s = 0; s < NQ; ++s)
+                            t = fma(hFu[s * NU + a], Gm[NQ + s][b], fma(Ps(NQ + s, NX + a), hFu[s * NU + b], t));
+                        if (a == b) t += R[a] + Rm[a];
+                        Hww[a][b] = t;
+                    }
+                    double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
+#pragma unroll
+                    for (int s = 0; s < NQ; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) t = fma(Ps(r, NX + a), cc[r], t);
+                    Y[a][NS] = t;
+                    double ga[NX];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) ga[r] = Gm[r][a];
+                    at_mul<NQ, double>(h, hFq, hFqd, ga, &Y[a][0]);
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) Y[a][NX + c] = (a == c) ? -R[a] : 0.0;
+                }
+                // P~_k x block A^T P_xx A + Q and p~_k x part A^T mv + Q (x_k - r_{k-1}), before P is overwritten
+                double Pn[NX][NX], pn[NS];
+                if (k >= 1) {
+#pragma unroll
+                    for (int b = 0; b < NX; ++b) {
+                        double row[NX], tcol[NX];
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) {
+                            double t;
+                            if (b < NQ) {
+                                t = Ps(r, b);
+#pragma unroll
+                                for (int s = 0; s < NQ; ++s) t = fma(hFq[s * NQ + b], Ps(r, NQ + s), t);
+                            } else {
+                                t = fma(h, Ps(r, b - NQ), Ps(r, b));
+#pragma unroll
+                                for (int s = 0; s < NQ; ++s) t = fma(hFqd[s * NQ + b - NQ], Ps(r, NQ + s), t);
+                            }
+                            tcol[r] = t;
+                        }
+                        at_mul<NQ, double>(h, hFq, hFqd, tcol, row);
+#pragma unroll
+                        for (int a = 0; a <= b; ++a) Pn[a][b] = row[a] + ((a == b) ? Q[a] : 0.0);
+                    }
+                    double t[NX];
+                    at_mul<NQ, double>(h, hFq, hFqd, mv, t);
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - tr[(k - 1) * NX + q], t[q]);
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
+                }
+                double Ld[NU][NU], il[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double sd = Hww[a][a];
+#pragma unroll
+                    for (int q = 0; q < a; ++q) sd = fma(-Ld[a][q], Ld[a][q], sd);
+                    fact_ok &= (sd > 0.0) && isfinite(sd);
+                    const double lj = sqrt(fmax(sd, 1e-300));
+                    Ld[a][a] = lj;
+                    il[a] = 1.0 / lj;
+#pragma unroll
+                    for (int b = a + 1; b < NU; ++b) {
+                        double t = Hww[a][b];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
+                        Ld[b][a] = t * il[a];
+                    }
+                }
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int j = 0; j <= NS; ++j) {
+                        double t = Y[a][j];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
+                        Y[a][j] = t * il[a];
+                    }
+                {
+                    double Kt[NU][NS + 1];
+#pragma unroll
+                    for (int a = NU - 1; a >= 0; --a)
+#pragma unroll
+                        for (int j = 0; j <= NS; ++j) {
+                            double t = Y[a][j];
+#pragma unroll
+                            for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], Kt[q][j], t);
+                            Kt[a][j] = t * il[a];
+                        }
+#pragma unroll
+                    for (int a = 0; a < NU; ++a)
+#pragma unroll
+                        for (int j = 0; j <= NS; ++j) wK[(k * NU + a) * (NS + 1) + j] = -Kt[a][j];
+                }
+                if (k == 0) break;
+#pragma unroll
+                for (int a = 0; a < NS; ++a) {
+                    double t = pn[a];
+#pragma unroll
+                    for (int q = 0; q < NU; ++q) t = fma(-Y[q][a], Y[q][NS], t);
+                    pv[a] = t;
+#pragma unroll
+                    for (int b = a; b < NS; ++b) {
+                        double v = (b < NX) ? Pn[a][b] : ((a == b) ? R[a - NX] : 0.0);
+#pragma unroll
+                        for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
+                        P[a][b] = v;
+                    }
+                }
+            }
+#undef Ps
+        }
+        gmax = group_bcast(gmax, gbase);
+        lmax = group_bcast(lmax, gbase);
+        fact_ok = group_bcast_i(fact_ok, gbase);
+        MMPC_PHASE(2);
+        nonfinite = (group_max((double)nonfinite) != 0.0);
+        kkt = fmax(gmax, cmax);
+        double* trc = p.trace && valid ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
+        if (trc && gl == 0) {
+            trc[0] = gmax;
+            trc[1] = cmax;
+            trc[2] = J0;
+            trc[3] = c1;
+            trc[7] = lmax;
+        }
+        if (nonfinite || !isfinite(kkt)) {
+            status = ST_NONFINITE;
+            break;
+        }
+        if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
+            status = ST_CONVERGED;
+            break;
+        }
+        if (it == p.max_iter) {
+            status = ST_MAX_ITER;
+            break;
+        }
+        if (!fact_ok) {
+            status = ST_FACT_FAILED;
+            break;
+        }
+
+        MMPC_PHASE(3);
+        // ---- C. one lane: step sweep du = K s + kff, dx, directional derivative ----
+        double dJ = 0.0;
+        if (gl == 0) {
+            double dx[NX], dup[NU], um[NU];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                dx[r] = 0.0;
+                sDX[r] = 0.0;
+            }
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                dup[c] = 0.0;
+                um[c] = up[c];
+            }
+            // software pipeline: K_{k+1} (HBM) and the LDS operands of step k+1 are loaded during step k
+            constexpr int NK = NU * (NS + 1);
+            double nK[NK], nFq[NQ * NQ], nFqd[NQ * NQ], nFu[NQ * NU], nF[NX], nc[NX], nr[NX], nu_[NU];
+#define GROUP_LOAD_STEP(k_)                                                                        \
+    do {                                                                                           \
+        const int kk_ = (k_);                                                                      \
+        _Pragma("unroll") for (int i_ = 0; i_ < NK; ++i_) nK[i_] = wK[kk_ * NK + i_];              \
+        _Pragma("unroll") for (int i_ = 0; i_ < NQ * NQ; ++i_) {                                   \
+            nFq[i_] = sFq[kk_ * NQ * NQ + i_];                                                     \
+            nFqd[i_] = sFqd[kk_ * NQ * NQ + i_];                                                   \
+        }                                                                                          \
+        _Pragma("unroll") for (int i_ = 0; i_ < NQ * NU; ++i_) nFu[i_] = sFu[kk_ * NQ * NU + i_];  \
+        _Pragma("unroll") for (int r_ = 0; r_ < NX; ++r_) {                                        \
+            nF[r_] = sF[kk_ * NX + r_];                                                            \
+            nc[r_] = sC[kk_ * NX + r_];                                                            \
+            nr[r_] = sR[kk_ * NX + r_];                                                            \
+        }                                                                                          \
+        _Pragma("unroll") for (int c_ = 0; c_ < NU; ++c_) nu_[c_] = sU[kk_ * NU + c_];             \
+    } while (0)
+            GROUP_LOAD_STEP(0);
+            for (int k = 0; k < N; ++k) {
+                double K[NK], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU], Fk[NX], ck[NX], rk[NX], uk[NU];
+#pragma unroll
+                for (int i = 0; i < NK; ++i) K[i] = nK[i];
+#pragma unroll
+                for (int i = 0; i < NQ * NQ; ++i) {
+                    hFq[i] = nFq[i];
+                    hFqd[i] = nFqd[i];
+                }
+#pragma unroll
+                for (int i = 0; i < NQ * NU; ++i) hFu[i] = nFu[i];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    Fk[r] = nF[r];
+                    ck[r] = nc[r];
+                    rk[r] = nr[r];
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) uk[c] = nu_[c];
+                if (k + 1 < N) GROUP_LOAD_STEP(k + 1);
+                double du[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double t = K[a * (NS + 1) + NS];
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) t = fma(K[a * (NS + 1) + q], dx[q], t);
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) t = fma(K[a * (NS + 1) + NX + c], dup[c], t);
+                    du[a] = t;
+                    sDU[k * NU + a] = t;
+                }
+                double ad[NX];
+                a_mul<NQ, double>(h, hFq, hFqd, dx, ad);
+#pragma unroll
+                for (int s = 0; s < NQ; ++s)
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    const double qe = 2.0 * Q[r] * (Fk[r] - rk[r]);
+                    dJ = fma(qe, ad[r], dJ);
+                    dx[r] = ad[r] + ck[r];
+                    sDX[(k + 1) * NX + r] = dx[r];
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const double dif = uk[c] - um[c];
+                    dJ = fma(2.0 * R[c] * dif, du[c] - dup[c], fma(2.0 * Rm[c] * uk[c], du[c], dJ));
+                    um[c] = uk[c];
+                    dup[c] = du[c];
+                }
+            }
+#undef GROUP_LOAD_STEP
+        }
+        dJ = group_bcast(dJ, gbase);
+        __builtin_amdgcn_wave_barrier();
+        MMPC_PHASE(4);
+
+        // ---- D. stage-parallel l1-merit Armijo line search (noise-aware, as sqp_wave.h), update ----
+        mu = fmax(mu, 4.0 * lmax + 1.0);
+        const double phi0 = fma(mu, c1, J0);
+        const double dphi = dJ - mu * c1;
+        double alpha = 1.0;
+        bool accepted = false;
+        for (int ls = 0; ls < 30; ++ls) {
+            double Jt = 0.0, ct = 0.0;
+            for (int k = gl; k < N; k += G) {
+                double x[NX], u[NU], xd[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) x[r] = fma(alpha, sDX[k * NX + r], sX[k * NX + r]);
+#pragma unroll
+                for (int c = 0; c < NU; ++c) u[c] = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
+                group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, nullptr, nullptr, nullptr, false);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    const double F = fma(h, xd[r], x[r]);
+                    const double er = F - tr[k * NX + r];
+                    Jt = fma(er * Q[r], er, Jt);
+                    ct += fabs(F - fma(alpha, sDX[(k + 1) * NX + r], sX[(k + 1) * NX + r]));
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const double um =
+                        (k == 0) ? up[c] : fma(alpha, sDU[(k - 1) * NU + c], sU[(k - 1) * NU + c]);
+                    const double dif = u[c] - um;
+                    Jt = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], Jt));
+                }
+            }
+            Jt = group_sum(Jt);
+            ct = group_sum(ct);
+            const double phit = fma(mu, ct, Jt);
+            const double noise = 1.0 + fabs(phi0);
+            if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) {
+                accepted = true;
+                break;
+            }
+            alpha *= 0.5;
+        }
+        if (trc && gl == 0) {
+            trc[4] = dJ;
+            trc[5] = alpha;
+            trc[6] = mu;
+        }
+        MMPC_PHASE(5);
+        if (!accepted) {
+            status = ST_LS_FAILED;
+            break;
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int k = gl; k <= N; k += G) {
+            if (k > 0) {
+#pragma unroll
+                for (int r = 0; r < NX; ++r) sX[k * NX + r] = fma(alpha, sDX[k * NX + r], sX[k * NX + r]);
+            }
+            if (k < N) {
+#pragma unroll
+                for (int c = 0; c < NU; ++c) sU[k * NU + c] = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    MMPC_PHASE(6);
+    if (!valid) return;
+    // ---- bounds check (reported, not enforced), as sqp_wave.h ----
+    if (status == ST_CONVERGED && (p.u_lb || p.u_ub)) {
+        bool viol = false;
+        for (int k = gl; k < N; k += G)
+#pragma unroll
+            for (int r = 0; r < NU; ++r) {
+                const double u = sU[k * NU + r];
+                if (p.u_lb) viol |= (p.u_lb[r] > -1e19) && (u < p.u_lb[r] - 1e-9);
+                if (p.u_ub) viol |= (p.u_ub[r] < 1e19) && (u > p.u_ub[r] + 1e-9);
+            }
+        if (group_max(viol ? 1.0 : 0.0) != 0.0) status = ST_BOUNDS;
+    }
+    // ---- write back V (reference layout), stage-parallel ----
+    double* Vout = p.V + inst * (int64_t)NV;
+    for (int k = gl; k <= N; k += G) {
+#pragma unroll
+        for (int r = 0; r < NX; ++r) Vout[k * ND + r] = sX[k * NX + r];
+        if (k < N) {
+#pragma unroll
+            for (int c = 0; c < NU; ++c) Vout[k * ND + NX + c] = sU[k * NU + c];
+        }
+    }
+    if (gl == 0) {
+        if (p.status) p.status[inst] = status;
+        if (p.iters) p.iters[inst] = it;
+        if (p.kkt) p.kkt[inst] = kkt;
+    }
+    MMPC_PHASE(7);
+    MMPC_PHASE_FLUSH
+}
+
+}  // namespace mmpc

@@ -39,7 +39,7 @@ class MmpcError(RuntimeError):
         self.code = code
 
 
-KKT_AUTO, KKT_CONDENSED, KKT_RICCATI = 0, 1, 2
+KKT_AUTO, KKT_CONDENSED, KKT_RICCATI, KKT_RICCATI_GROUP = 0, 1, 2, 3
 MODEL_TWO_LINK_ARM, MODEL_EXO_ARM = 0, 1
 
 

@@ -254,3 +254,59 @@ def test_fp32_factor_is_riccati_only(model_json, mmpc_mod, oracle):
     with pytest.raises(mmpc_mod.MmpcError) as ei:
         s.solve_batch_host(x0, up, tr, np.array(WEIGHTS_CFG))
     assert ei.value.code == -4
+
+
+# ---- 16-lanes-per-instance Riccati kernel (sqp_group.h) ----
+@pytest.mark.parametrize("N,B", [(30, 512), (1, 5), (7, 70), (33, 65), (50, 64)])
+def test_group_kernel_vs_oracle(N, B, model_json, mmpc_mod, oracle):
+    x0, up, tr = oracle.synth(20250213, 3, B, N, H)
+    w = np.array(WEIGHTS_CFG)
+    r = mmpc_mod.Solver(model_json(N=N), kkt_solver=mmpc_mod.KKT_RICCATI_GROUP).solve_batch_host(x0, up, tr, w)
+    o = oracle.solve_batch(N, H, x0, up, tr, w)
+    _compare(r, o)
+
+
+def test_group_kernel_linear_weights_bounds_nonfinite_warmstart(model_json, mmpc_mod, oracle):
+    G = mmpc_mod.KKT_RICCATI_GROUP
+    x0, up, tr = oracle.synth(11, 0, 64, 25, H)
+    w = np.array(WEIGHTS_CFG)
+    s = mmpc_mod.Solver(model_json(N=25, name="linear_double_pendulum", is_linear=True), kkt_solver=G)
+    r = s.solve_batch_host(x0, up, tr, w)
+    assert (r["iters"] == 1).all()
+    _compare(r, oracle.solve_batch(25, H, x0, up, tr, w, is_linear=True), min_same=1.0)
+    x0, up, tr = oracle.synth(13, 0, 64, 30, H)
+    rng = np.random.default_rng(0)
+    wi = np.tile(WEIGHTS_CFG, (64, 1)) * rng.uniform(0.5, 2.0, (64, 8))
+    s = mmpc_mod.Solver(model_json(N=30), kkt_solver=G)
+    r = s.solve_batch_host(x0, up, tr, wi)
+    _compare(r, oracle.solve_batch(30, H, x0, up, tr, wi))
+    r2 = s.solve_batch_host(x0, up, tr, wi, V=r["V"])
+    assert (r2["iters"] == 0).all() and (r2["status"] == 0).all()
+    np.testing.assert_array_equal(r2["V"], r["V"])
+    r3 = s.solve_batch_host(x0[:8], up[:8], tr[:8], w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
+    o3 = oracle.solve_batch(30, H, x0[:8], up[:8], tr[:8], w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
+    np.testing.assert_array_equal(r3["status"], o3["status"])
+    x0b, trb = x0[:4].copy(), tr[:4].copy()
+    x0b[1, 0] = np.nan
+    trb[2, 3, 1] = np.inf
+    r4 = s.solve_batch_host(x0b, up[:4], trb, w)
+    assert list(r4["status"]) == [0, 3, 3, 0]
+
+
+@pytest.mark.parametrize("N,B", [(20, 70), (5, 9), (40, 64)])
+def test_group_kernel_exo_vs_oracle(N, B, exo_solver, mmpc_mod, oracle):
+    # explicit request (AUTO keeps exo on the lane kernel); stage data fits LDS up to N = 47
+    x0, up, tr = oracle.synth(20250213, 7, B, N, H, model=oracle.EXO)
+    r = exo_solver(N=N, kkt_solver=mmpc_mod.KKT_RICCATI_GROUP).solve_batch_host(x0, up, tr, W_EXO)
+    o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, model=oracle.EXO)
+    _compare(r, o)
+
+
+def test_group_kernel_exo_lds_limit(exo_solver, mmpc_mod, oracle):
+    # N = 50 exceeds 160 KB of LDS for 4 exo instances: explicit request fails, AUTO uses lanes
+    x0, up, tr = oracle.synth(1, 0, 4, 50, H, model=oracle.EXO)
+    with pytest.raises(mmpc_mod.MmpcError) as ei:
+        exo_solver(N=50, kkt_solver=mmpc_mod.KKT_RICCATI_GROUP).solve_batch_host(x0, up, tr, W_EXO)
+    assert ei.value.code == -4
+    r = exo_solver(N=50).solve_batch_host(x0, up, tr, W_EXO)
+    assert (r["status"] == 0).all()

@@ -35,7 +35,11 @@ L = mmpc.lib()
 L.mmpc_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
 path = mmpc.write_model_json("/tmp/mmpc_phase.json", "phase", nx, nu, 2000, N)
 s = mmpc.Solver(path, kkt_solver=a.kkt)
-if exo or a.kkt == 2 or N * nu > 64:
+NAMES_GROUP = ["load", "A:evals(parallel)", "B:d+backward(serial)", "check", "C:step(serial)", "D:line_search",
+               "update+after_loop", "writeback", "-", "-"]
+if a.kkt == 3:
+    NAMES = NAMES_GROUP
+elif exo or a.kkt == 2 or N * nu > 64:
     NAMES = NAMES_LANE
 f = dict(dtype=torch.float64, device="cuda")
 x0 = torch.empty((B, nx), **f); up = torch.empty((B, nu), **f); tr = torch.empty((B, N, nx), **f)
