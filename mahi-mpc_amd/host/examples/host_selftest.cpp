@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <stdexcept>
+#include <utility>
 
 #include "../../../include/mmpc.h"
 
@@ -37,6 +38,30 @@ int main() {
     mmpc_model_info info;
     CHECK(mmpc_get_model_info(h, &info) == MMPC_OK && info.num_shooting_nodes == 25 && info.num_v == 154);
     mmpc_destroy(h);
+    // CasADi-external linear functions (ModelGenerator.cpp:45-53,241-251): metadata only, no GPU call
+    for (const char* fn : {"_get_A", "_get_B", "_get_x_dot_init"}) {
+        External e = external(std::string("selftest_double_pendulum") + fn, "selftest_double_pendulum_linear_functions.so");
+        CHECK(e.n_in() == 2 && e.n_out() == 1);
+        CHECK(e.size_in(0) == std::make_pair(4LL, 1LL) && e.size_in(1) == std::make_pair(2LL, 1LL));
+    }
+    CHECK(external("selftest_double_pendulum_get_A", "selftest_double_pendulum_linear_functions.so").size_out(0) ==
+          std::make_pair(4LL, 4LL));
+    CHECK(external("selftest_double_pendulum_get_B", "selftest_double_pendulum_linear_functions.so").size_out(0) ==
+          std::make_pair(4LL, 2LL));
+    {
+        ModelGenerator exo(ModelParameters("selftest_exo", 8, 4, mahi::util::milliseconds(2), 50, false), "exo_arm");
+        exo.create_model();
+        exo.compile_model();
+        External e = external("selftest_exo_get_B", "selftest_exo_linear_functions.so");
+        CHECK(e.size_in(0) == std::make_pair(8LL, 1LL) && e.size_out(0) == std::make_pair(8LL, 4LL));
+        bool bad_size = false;
+        try {
+            e({std::vector<double>(8, 0.0), std::vector<double>(3, 0.0)});
+        } catch (const std::invalid_argument&) {
+            bad_size = true;
+        }
+        CHECK(bad_size);
+    }
     bool threw = false;
     try {
         ModelGenerator bad(ModelParameters("bad", 8, 4, mahi::util::milliseconds(2), 10, false), "two_link_arm");

@@ -2,7 +2,8 @@
 // with the thread example's weights (thread_model_control_example.cpp:24-25) and an explicit Rm.
 // ModelGenerator writes the model file (ex_model_generate.cpp:59-71 with N from the command line), then
 // calc_u runs every 5th tick (model_control_example.cpp:74-76) and the Euler plant uses the device
-// linearisation's x_dot (model_control_example.cpp:81-86).  Prints one CSV line per tick:
+// linearisation's x_dot through <name>_get_x_dot_init of the generated <name>_linear_functions.so
+// (model_control_example.cpp:46,81-86).  Prints one CSV line per tick:
 //   t, q0..q3, T0, T1, status, iterations
 #include <Mahi/Mpc.hpp>
 
@@ -30,8 +31,8 @@ int main(int argc, char** argv) {
     const int nx = mc.model_parameters.num_x;
     const double h = mc.model_parameters.step_size.as_seconds();
     std::vector<double> state(4, 0.0), control(2, 0.0);
-    mmpc_handle* lin = nullptr;  // plant model: <name>_get_x_dot_init replacement
-    if (mmpc_create((name + ".json").c_str(), nullptr, &lin) != MMPC_OK) return 2;
+    // plant model through the generated CasADi external, as model_control_example.cpp:46
+    auto ext_x_dot_init = external(name + "_get_x_dot_init", name + "_linear_functions.so");
     const double PI = 3.14159265358979323846, sin_amp = 1.0, sin_freq = 1.0;
     double t = 0.0;
     int cycle = 0;
@@ -47,14 +48,12 @@ int main(int argc, char** argv) {
         }
         if (cycle % 5 == 0) mc.calc_u(mahi::util::seconds(t), state, control, traj);
         control = mc.control_at_time(mahi::util::seconds(t)).u;
-        double xd[4];
-        if (mmpc_linearize_batch_host(lin, 1, state.data(), control.data(), nullptr, nullptr, xd) != MMPC_OK) return 3;
+        std::vector<double> xd(ext_x_dot_init({state, control})[0]);  // model_control_example.cpp:81-82
         std::printf("%.6f,%.17g,%.17g,%.17g,%.17g,%.17g,%.17g,%d,%d\n", t, state[0], state[1], state[2], state[3],
                     control[0], control[1], mc.last_status(), mc.last_iterations());
         for (int i = 0; i < 4; i++) state[i] += xd[i] * h;
         t += h;
         cycle++;
     }
-    mmpc_destroy(lin);
     return 0;
 }

@@ -13,10 +13,12 @@ namespace mpc {
 
 class ModelGenerator {
 public:
-    // dynamics: name of a built-in model ("two_link_arm" == examples/ex_model_generate.cpp:24-43)
+    // dynamics: name of a built-in model ("two_link_arm" == examples/ex_model_generate.cpp:24-43, "exo_arm")
     ModelGenerator(ModelParameters model_parameters, std::string dynamics = "two_link_arm");
     ~ModelGenerator();
-    void create_model();      // validates dimensions against the built-in model
+    void create_model();      // validates dimensions, then generate_linear_functions()
+    // <name>_linear_functions.{c,so}: <name>_get_A/_get_B/_get_x_dot_init with the CasADi external ABI
+    void generate_linear_functions();
     void generate_c_code();   // nothing to generate: the device code is compiled into libmmpc.so
     void compile_model();     // sets dll_filepath to libmmpc.so and writes <name>.json
     void save_param_file();   // <name>.json (ModelGenerator.cpp:261-270)

@@ -68,3 +68,47 @@ def test_closed_loop_example_matches_oracle(linear, oracle, tmp_path):
     assert rows.shape == ref.shape, (rows.shape, ref.shape)
     assert (rows[:, 7] == 0).all()                                  # every GPU solve converged
     np.testing.assert_allclose(rows[:, 1:7], ref[:, 1:7], rtol=1e-7, atol=1e-9)
+
+
+def test_generated_linear_functions_casadi_abi(golden_kat, oracle, mmpc_mod, tmp_path):
+    """<name>_get_A/_get_B/_get_x_dot_init of the generated <name>_linear_functions.so, called through the CasADi
+    external C ABI (src/codegen_usage.cpp:73-181) with ctypes: CasADi column-major outputs equal to the device
+    linearisation bit for bit, and to the sympy K2/K3 fixtures (2-link, 1e-11) / the oracle (exo, 1e-12)."""
+    import ctypes as C
+    subprocess.run(["make", "-s", "-C", HOST], check=True)
+    out = subprocess.run([os.path.join(HOST, "bin", "host_selftest")], cwd=tmp_path, capture_output=True, text=True)
+    assert out.returncode == 0, out.stdout + out.stderr
+    dp = lambda a: a.ctypes.data_as(C.POINTER(C.c_double))  # noqa: E731
+
+    def call(lib, fn, x, u, nout):
+        f = getattr(lib, fn)
+        f.restype = C.c_int
+        arg = (C.POINTER(C.c_double) * 2)(dp(x), dp(u))
+        r = np.full(nout, np.nan)
+        res = (C.POINTER(C.c_double) * 1)(dp(r))
+        assert f(arg, res, None, None, 0) == 0
+        return r
+
+    rng = np.random.default_rng(3)
+    for name, nx, nu in (("selftest_double_pendulum", 4, 2), ("selftest_exo", 8, 4)):
+        lib = C.CDLL(str(tmp_path / f"{name}_linear_functions.so"))
+        s = mmpc_mod.Solver(str(tmp_path / f"{name}.json"))
+        if nx == 4:
+            pts = [(np.array(p["x"], float), np.array(p["u"], float), np.array(p["A"]), np.array(p["B"]), 1e-11)
+                   for p in golden_kat["K3"]["points"]]
+        else:
+            pts = []
+            for _ in range(4):
+                x, u = rng.uniform(-1, 1, nx), rng.uniform(-2, 2, nu)
+                Ao, Bo, _ = oracle.exo_jac(x, u)
+                pts.append((x, u, Ao, Bo, 1e-12))
+        for x, u, Aref, Bref, tol in pts:
+            A = call(lib, name + "_get_A", x, u, nx * nx).reshape(nx, nx).T   # column-major -> row-major
+            Bm = call(lib, name + "_get_B", x, u, nx * nu).reshape(nu, nx).T
+            xd = call(lib, name + "_get_x_dot_init", x, u, nx)
+            Ad, Bd, xdd = s.linearize_host(x[None], u[None])
+            np.testing.assert_array_equal(A, Ad[0])
+            np.testing.assert_array_equal(Bm, Bd[0])
+            np.testing.assert_array_equal(xd, xdd[0])
+            np.testing.assert_allclose(A, Aref, rtol=tol, atol=tol * np.abs(Aref).max())
+            np.testing.assert_allclose(Bm, Bref, rtol=tol, atol=tol * np.abs(Bref).max())
