@@ -286,7 +286,7 @@ void oracle_reduced_gradient(int model, int N, double h, const double* x0, const
 /* ---------------- dense GN-SQP for one instance ---------------- */
 typedef struct {
     int N, M;
-    double *X, *U, *F, *Ad, *Bd, *c, *d, *e, *G, *H, *g, *du, *dx, *lam, *Xt, *Ut, *Ft;
+    double *X, *U, *F, *Ad, *Bd, *c, *d, *e, *G, *H, *g, *du, *dx, *lam, *Xt, *Ut, *Ft, *H0, *g0, *tgt;
 } ws_t;
 
 static void ws_alloc(ws_t* s, int N) {
@@ -309,11 +309,14 @@ static void ws_alloc(ws_t* s, int N) {
     s->Xt = calloc((size_t)(N + 1) * NX, sizeof(double));
     s->Ut = calloc((size_t)N * NU, sizeof(double));
     s->Ft = calloc((size_t)N * NX, sizeof(double));
+    s->H0 = calloc(M * M, sizeof(double));
+    s->g0 = calloc(M, sizeof(double));
+    s->tgt = calloc(M, sizeof(double));
 }
 static void ws_free(ws_t* s) {
     free(s->X); free(s->U); free(s->F); free(s->Ad); free(s->Bd); free(s->c); free(s->d);
     free(s->e); free(s->G); free(s->H); free(s->g); free(s->du); free(s->dx); free(s->lam);
-    free(s->Xt); free(s->Ut); free(s->Ft);
+    free(s->Xt); free(s->Ut); free(s->Ft); free(s->H0); free(s->g0); free(s->tgt);
 }
 
 /* merit pieces at (X,U): J and sum |c| (F returned) */
@@ -376,6 +379,20 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
     }
     memcpy(s->X + N * NX, V + N * ND, sizeof(double) * NX);
     memcpy(s->X, x0, sizeof(double) * NX);
+    /* box constraints on u (ModelControl.cpp:37-50,146-157; |b| >= 1e19 is unbounded, as IPOPT): projected
+     * Gauss-Newton SQP -- the iterate starts projected, controls at a bound whose gradient points outward
+     * (epsilon-active set, Bertsekas 1982) are held in the QP, trial points are projected onto the box and the
+     * stop test uses the projected gradient ||U - P(U - 2g)||_inf. */
+    double lbv[4], ubv[4];
+    int has_b = 0;
+    for (int q = 0; q < NU; ++q) {
+        lbv[q] = (u_lb && u_lb[q] > -1e19) ? u_lb[q] : -INFINITY;
+        ubv[q] = (u_ub && u_ub[q] < 1e19) ? u_ub[q] : INFINITY;
+        has_b |= (lbv[q] > -INFINITY) || (ubv[q] < INFINITY);
+    }
+    if (has_b)
+        for (int a = 0; a < M; ++a) s->U[a] = fmin(fmax(s->U[a], lbv[a % NU]), ubv[a % NU]);
+    double pg_prev = INFINITY;
 
     int status = ORACLE_MAX_ITER, it = 0;
     double kkt = INFINITY, mu = 0.0;
@@ -443,7 +460,21 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
             }
         }
         double gmax = 0.0;
-        for (int a = 0; a < M; ++a) { double t = fabs(2.0 * s->g[a]); if (t > gmax || t != t) gmax = t; }
+        if (!has_b) {
+            for (int a = 0; a < M; ++a) { double t = fabs(2.0 * s->g[a]); if (t > gmax || t != t) gmax = t; }
+        } else {
+            /* epsilon-active set (Bertsekas 1982) from the previous iteration's projected gradient: the
+             * Riccati kernels decide a stage's set inside the backward sweep that computes this iteration's
+             * gradient.  A held control is fixed at its bound in the QP (du_a = bound - u_a). */
+            const double eps = fmin(ORACLE_BOUND_EPS, pg_prev);
+            for (int a = 0; a < M; ++a) {
+                const double u = s->U[a], lb = lbv[a % NU], ub = ubv[a % NU];
+                double t = fabs(u - fmin(fmax(u - 2.0 * s->g[a], lb), ub));
+                if (t > gmax || t != t) gmax = t;
+                s->tgt[a] = (u <= lb + eps && s->g[a] > 0.0) ? lb : (u >= ub - eps && s->g[a] < 0.0) ? ub : NAN;
+            }
+            pg_prev = gmax;
+        }
         kkt = gmax > cmax ? gmax : cmax;
         if (!isfinite(kkt)) { status = ORACLE_NONFINITE; break; }
         if (gmax <= tol_grad && cmax <= tol_defect) { status = ORACLE_CONVERGED; break; }
@@ -462,9 +493,40 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
             }
         }
 
-        /* (6) step: Cholesky of H, du = -H^-1 g; dx_0 = 0, dx_{k+1} = A dx + B du + c */
-        for (int a = 0; a < M; ++a) s->du[a] = -s->g[a];
-        if (chol_solve(M, s->H, s->du) != 0) { status = ORACLE_FACTORIZATION_FAILED; break; }
+        /* (6) step: Cholesky of H, du = -H^-1 g; dx_0 = 0, dx_{k+1} = A dx + B du + c.
+         * With bounds: the equality-constrained QP with du_a = tgt_a - u_a for the held controls; a free control
+         * whose step leaves the box is then held at the bound it crosses and the QP solved again (at most
+         * ORACLE_BOUND_PASSES solves; the projected line search absorbs what is left). */
+        int fact_fail = 0;
+        if (has_b) { memcpy(s->H0, s->H, sizeof(double) * M * M); memcpy(s->g0, s->g, sizeof(double) * M); }
+        for (int pass = 0;; ++pass) {
+            if (has_b) {
+                if (pass) memcpy(s->H, s->H0, sizeof(double) * M * M);
+                for (int a = 0; a < M; ++a) s->g[a] = s->g0[a];
+                for (int a = 0; a < M; ++a) {
+                    if (s->tgt[a] != s->tgt[a]) continue;
+                    const double da = s->tgt[a] - s->U[a];
+                    for (int b = 0; b < M; ++b) {
+                        s->g[b] += s->H0[b * M + a] * da;
+                        s->H[a * M + b] = s->H[b * M + a] = 0.0;
+                    }
+                }
+                for (int a = 0; a < M; ++a)
+                    if (s->tgt[a] == s->tgt[a]) { s->H[a * M + a] = 1.0; s->g[a] = s->U[a] - s->tgt[a]; }
+            }
+            for (int a = 0; a < M; ++a) s->du[a] = -s->g[a];
+            if (chol_solve(M, s->H, s->du) != 0) { fact_fail = 1; break; }
+            if (!has_b || pass + 1 >= ORACLE_BOUND_PASSES) break;
+            int added = 0;
+            for (int a = 0; a < M; ++a) {
+                if (s->tgt[a] == s->tgt[a]) continue;
+                const double t = s->U[a] + s->du[a];
+                if (t < lbv[a % NU]) { s->tgt[a] = lbv[a % NU]; added = 1; }
+                else if (t > ubv[a % NU]) { s->tgt[a] = ubv[a % NU]; added = 1; }
+            }
+            if (!added) break;
+        }
+        if (fact_fail) { status = ORACLE_FACTORIZATION_FAILED; break; }
         memset(s->dx, 0, sizeof(double) * NX);
         for (int k = 0; k < N; ++k)
             for (int r = 0; r < NX; ++r) {
@@ -506,6 +568,8 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         for (int ls = 0; ls < 30; ++ls) {
             for (int i = 0; i < (N + 1) * NX; ++i) s->Xt[i] = s->X[i] + alpha * s->dx[i];
             for (int i = 0; i < M; ++i) s->Ut[i] = s->U[i] + alpha * s->du[i];
+            if (has_b)  /* projected trial point */
+                for (int i = 0; i < M; ++i) s->Ut[i] = fmin(fmax(s->Ut[i], lbv[i % NU]), ubv[i % NU]);
             double Jt, ct;
             merit_eval(N, h, s->Xt, s->Ut, u_prev, traj, w, s->Ft, &Jt, &ct);
             double phit = Jt + mu * ct;
@@ -525,14 +589,6 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         memcpy(V + k * ND + NX, s->U + k * NU, sizeof(double) * NU);
     }
     memcpy(V + N * ND, s->X + N * NX, sizeof(double) * NX);
-    if (status == ORACLE_CONVERGED && (u_lb || u_ub)) {
-        for (int k = 0; k < N; ++k)
-            for (int q = 0; q < NU; ++q) {
-                double u = s->U[k * NU + q];
-                if ((u_lb && u_lb[q] > -1e19 && u < u_lb[q] - 1e-9) || (u_ub && u_ub[q] < 1e19 && u > u_ub[q] + 1e-9))
-                    status = ORACLE_BOUNDS_VIOLATED;
-            }
-    }
     if (J_out) {
         double J;
         oracle_nlp_eval(t_model, N, h, V, u_prev, traj, w, &J, NULL);

@@ -31,8 +31,12 @@ enum {
     ORACLE_LINESEARCH_FAILED = 2,
     ORACLE_NONFINITE = 3,
     ORACLE_FACTORIZATION_FAILED = 4,
-    ORACLE_BOUNDS_VIOLATED = 5
+    ORACLE_BOUNDS_VIOLATED = 5  /* reserved: u bounds are enforced (projected GN-SQP), never reported */
 };
+/* epsilon of the epsilon-active set of the bound-constrained solve: min(ORACLE_BOUND_EPS, previous ||pg||) */
+#define ORACLE_BOUND_EPS 1e-6
+/* QP solves per SQP iteration with bounds: the first, plus re-solves after holding crossed bounds */
+#define ORACLE_BOUND_PASSES 4
 
 /* x_dot = f(x,u) of the 2-link arm, examples/ex_model_generate.cpp:24-43 */
 void oracle_two_link_xdot(const double* x, const double* u, double* xdot);

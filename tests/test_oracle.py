@@ -115,15 +115,18 @@ def test_linear_mode_single_iteration(oracle):
     assert (r["status"] == 0).all() and (r["iters"] == 1).all()
 
 
-def test_bounds_reported(oracle):
+def test_bounds_enforced(oracle):
+    """u bounds are enforced (projected GN-SQP, tests/test_oracle_bounds.py); status 5 is never produced"""
     x0, up, tr = oracle.synth(20250213, 0, 4, 30, 0.002)
     w = np.array(WEIGHTS_CFG)
     r = oracle.solve_batch(30, 0.002, x0, up, tr, w)
     umax = np.abs(r["V"][:, [6 * k + 4 + c for k in range(30) for c in range(2)]]).max()
     loose = oracle.solve_batch(30, 0.002, x0, up, tr, w, u_lb=[-1e31, -1e31], u_ub=[2 * umax, 2 * umax])
     assert (loose["status"] == 0).all()
+    np.testing.assert_array_equal(loose["V"], r["V"])     # inactive bounds: the unconstrained iterates
     tight = oracle.solve_batch(30, 0.002, x0, up, tr, w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
-    assert (tight["status"] == 5).all()
+    assert (tight["status"] == 0).all()
+    assert np.abs(tight["V"][:, [6 * k + 4 + c for k in range(30) for c in range(2)]]).max() <= 1e-3
 
 
 def test_nonfinite_input(oracle):
