@@ -80,8 +80,8 @@ enum mmpc_status {
     MMPC_STATUS_LINESEARCH_FAILED = 2,    /* no sufficient merit decrease after 30 halvings */
     MMPC_STATUS_NONFINITE = 3,            /* NaN/Inf in the iterate or the KKT residual */
     MMPC_STATUS_FACTORIZATION_FAILED = 4, /* condensed Hessian not positive definite */
-    MMPC_STATUS_BOUNDS_VIOLATED = 5       /* converged, but the solution leaves a finite u bound
-                                             (box constraints are not active-set handled yet) */
+    MMPC_STATUS_BOUNDS_VIOLATED = 5       /* reserved (ABI 1 reported violated u bounds); u bounds are
+                                             now enforced and this status is never produced */
 };
 
 /* built-in dynamics (device code; see DESIGN.md "Models") */
@@ -139,7 +139,9 @@ int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts);
 int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes);
 
 /* Batched SQP solve, DEVICE pointers, stream-ordered.  u_lb/u_ub: device [nu] or NULL
- * (unbounded; |bound| >= 1e19 is unbounded as in IPOPT).  status/iters/kkt_res: device
+ * (unbounded; |bound| >= 1e19 is unbounded as in IPOPT).  Finite bounds are enforced (the lbx/ubx
+ * of ModelControl.cpp:146-157): projected Gauss-Newton SQP, every returned u_k inside [u_lb, u_ub],
+ * kkt_res = max(||U - P(U - grad)||_inf, ||g||_inf).  status/iters/kkt_res: device
  * [B] outputs, each may be NULL. */
 int mmpc_solve_batch(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev,
                      const double* traj, const double* weights, int64_t weights_stride,

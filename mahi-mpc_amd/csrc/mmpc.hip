@@ -369,6 +369,20 @@ int set_dynamic_lds(K kernel, size_t bytes) {
     return MMPC_OK;
 }
 
+template <class Model, bool BOUNDED>
+int launch_group(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const SolveParams& p, GroupWork gwk) {
+    int rc = set_dynamic_lds(sqp_group_kernel<Model, BOUNDED>, lds);
+    if (rc) return rc;
+    sqp_group_kernel<Model, BOUNDED><<<grid, block, lds, stream>>>(p, gwk);
+    return MMPC_OK;
+}
+
+template <class Model, class FT>
+void launch_lane(bool bounded, dim3 grid, dim3 block, hipStream_t stream, const SolveParams& p, LaneWork lw) {
+    if (bounded) sqp_lane_kernel<Model, FT, true><<<grid, block, 0, stream>>>(p, lw);
+    else sqp_lane_kernel<Model, FT, false><<<grid, block, 0, stream>>>(p, lw);
+}
+
 // Riccati workspace (sqp_lane.h / sqp_group.h layouts), grown on demand.  Growth is synchronous:
 // hipFree waits for the kernels still using the old buffer.
 int ensure_workspace_bytes(mmpc_handle* h, size_t bytes, double** out) {
@@ -422,6 +436,9 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.kkt = kkt;
     p.trace = trace;
     const int N = mi.num_shooting_nodes;
+    // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
+    // points pass NULL for bounds that are all infinite
+    const bool bounded = u_lb || u_ub;
     int solver = h->opts.kkt_solver;
     const bool condensed_ok = mi.model_id == MMPC_MODEL_TWO_LINK_ARM && N * TwoLinkArm::NU <= 64;
     if (solver == MMPC_KKT_AUTO) {
@@ -443,13 +460,13 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
         if (rc) return rc;
         GroupWork gwk{lw.ws};
         dim3 grid(grid1d(B, kGroupsPerWave)), block(64);
-        if (mi.model_id == MMPC_MODEL_EXO_ARM) {
-            if ((rc = set_dynamic_lds(sqp_group_kernel<ExoArm>, lds))) return rc;
-            sqp_group_kernel<ExoArm><<<grid, block, lds, stream>>>(p, gwk);
-        } else {
-            if ((rc = set_dynamic_lds(sqp_group_kernel<TwoLinkArm>, lds))) return rc;
-            sqp_group_kernel<TwoLinkArm><<<grid, block, lds, stream>>>(p, gwk);
-        }
+        if (mi.model_id == MMPC_MODEL_EXO_ARM)
+            rc = bounded ? launch_group<ExoArm, true>(grid, block, lds, stream, p, gwk)
+                         : launch_group<ExoArm, false>(grid, block, lds, stream, p, gwk);
+        else
+            rc = bounded ? launch_group<TwoLinkArm, true>(grid, block, lds, stream, p, gwk)
+                         : launch_group<TwoLinkArm, false>(grid, block, lds, stream, p, gwk);
+        if (rc) return rc;
         MMPC_HIP(hipGetLastError());
         return MMPC_OK;
     }
@@ -459,9 +476,15 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
         if (!condensed_ok)
             return fail(MMPC_ERR_UNSUPPORTED, "condensed solver needs the 2-link arm and N*nu <= 64");
         dim3 grid(static_cast<unsigned>(B)), block(64);
-        if (N <= 16) sqp_wave_kernel<TwoLinkArm, 16><<<grid, block, 0, stream>>>(p);
-        else if (N <= 30) sqp_wave_kernel<TwoLinkArm, 30><<<grid, block, 0, stream>>>(p);
-        else sqp_wave_kernel<TwoLinkArm, 32><<<grid, block, 0, stream>>>(p);
+        if (bounded) {
+            if (N <= 16) sqp_wave_kernel<TwoLinkArm, 16, true><<<grid, block, 0, stream>>>(p);
+            else if (N <= 30) sqp_wave_kernel<TwoLinkArm, 30, true><<<grid, block, 0, stream>>>(p);
+            else sqp_wave_kernel<TwoLinkArm, 32, true><<<grid, block, 0, stream>>>(p);
+        } else {
+            if (N <= 16) sqp_wave_kernel<TwoLinkArm, 16><<<grid, block, 0, stream>>>(p);
+            else if (N <= 30) sqp_wave_kernel<TwoLinkArm, 30><<<grid, block, 0, stream>>>(p);
+            else sqp_wave_kernel<TwoLinkArm, 32><<<grid, block, 0, stream>>>(p);
+        }
     } else {
         LaneWork lw;
         int rc = ensure_workspace(h, B, &lw);
@@ -469,11 +492,11 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
         dim3 grid(grid1d(B, 64)), block(64);
         const bool f32 = h->opts.factor_fp32 != 0;
         if (mi.model_id == MMPC_MODEL_EXO_ARM) {
-            if (f32) sqp_lane_kernel<ExoArm, float><<<grid, block, 0, stream>>>(p, lw);
-            else sqp_lane_kernel<ExoArm, double><<<grid, block, 0, stream>>>(p, lw);
+            if (f32) launch_lane<ExoArm, float>(bounded, grid, block, stream, p, lw);
+            else launch_lane<ExoArm, double>(bounded, grid, block, stream, p, lw);
         } else {
-            if (f32) sqp_lane_kernel<TwoLinkArm, float><<<grid, block, 0, stream>>>(p, lw);
-            else sqp_lane_kernel<TwoLinkArm, double><<<grid, block, 0, stream>>>(p, lw);
+            if (f32) launch_lane<TwoLinkArm, float>(bounded, grid, block, stream, p, lw);
+            else launch_lane<TwoLinkArm, double>(bounded, grid, block, stream, p, lw);
         }
     }
     MMPC_HIP(hipGetLastError());
@@ -615,6 +638,13 @@ int mmpc_solve_batch_host(mmpc_handle* h, int64_t B, const double* x0, const dou
     std::lock_guard<std::mutex> lk(h->host_mu);
     const mmpc_model_info& mi = h->info;
     const size_t nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes, NV = mi.num_v;
+    // bounds that are all infinite (|b| >= 1e19, the reference's +-1e31 defaults) select the unbounded kernels
+    bool lb_finite = false, ub_finite = false;
+    for (size_t c = 0; c < nu; ++c) {
+        lb_finite |= u_lb && u_lb[c] > -1e19;
+        ub_finite |= u_ub && u_ub[c] < 1e19;
+    }
+    if (!lb_finite && !ub_finite) u_lb = u_ub = nullptr;
     const size_t nw = nx + 2 * nu;
     const size_t nW = weights_stride ? (size_t)B * (size_t)weights_stride : nw;
     // doubles: x0, u_prev, traj, weights, lb, ub, V, kkt ; ints: status, iters (as doubles' room)

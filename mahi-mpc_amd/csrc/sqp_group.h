@@ -25,7 +25,7 @@ constexpr int kGroupsPerWave = 4;
 
 // LDS doubles per instance
 __host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int N) {
-    return N * (3 * nx + 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + nu + nu) + 3 * (N + 1) * nx;
+    return N * (3 * nx + 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + 3 * nu) + 3 * (N + 1) * nx;
 }
 // HBM workspace doubles per instance: K_k | kff_k per stage
 __host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) { return N * nu * (nx + nu + 1); }
@@ -87,7 +87,7 @@ __device__ __forceinline__ void group_model(bool lin, const double* lFq, const d
     }
 }
 
-template <class Model>
+template <class Model, bool BOUNDED = false>
 __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork gw) {
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NS = NX + NU, ND = NX + NU;
     constexpr int G = kGroupLanes;
@@ -116,6 +116,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const sFqd = sFq + N * NQ * NQ;                        // [N][NQ*NQ]   h dacc/dqd
     double* const sFu = sFqd + N * NQ * NQ;                        // [N][NQ*NU]   h dacc/du
     double* const sR = sFu + N * NQ * NU;                          // [N][NX]      targets r_k
+    double* const sHold = sR + N * NX;                             // [N][NU]      bound a control is held at
     double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
     const double* const trg = p.traj + ii * (int64_t)N * NX;
 
@@ -129,6 +130,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         Rm[c] = w[NX + NU + c];
         up[c] = p.u_prev[ii * NU + c];
     }
+    double lbv[NU], ubv[NU];
+    load_bounds<NU, BOUNDED>(p, lbv, ubv);
     // ---- load: V (reference layout) -> LDS, x_0 pinned (ModelControl.cpp:144-145) ----
     {
         const double* Vin = p.V + ii * (int64_t)NV;
@@ -137,7 +140,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             for (int r = 0; r < NX; ++r) sX[k * NX + r] = (k == 0) ? p.x0[ii * NX + r] : Vin[k * ND + r];
             if (k < N) {
 #pragma unroll
-                for (int c = 0; c < NU; ++c) sU[k * NU + c] = Vin[k * ND + NX + c];
+                for (int c = 0; c < NU; ++c)
+                    sU[k * NU + c] = BOUNDED ? proj(Vin[k * ND + NX + c], lbv[c], ubv[c]) : Vin[k * ND + NX + c];
 #pragma unroll
                 for (int r = 0; r < NX; ++r) sR[k * NX + r] = trg[k * NX + r];
             }
@@ -160,7 +164,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     }
     int status = ST_MAX_ITER;
     int it = 0;
-    double kkt = 0.0, mu = 0.0;
+    double kkt = 0.0, mu = 0.0, pg_prev = INFINITY;
     bool done = !valid;
     MMPC_PHASE(0);
     for (it = 0; !done; ++it) {
@@ -211,24 +215,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         //      Riccati step of one stage is too small to pay for lane-parallel exchanges: measured slower) ----
         double gmax = 0.0, lmax = 0.0;
         int fact_ok = 1;
-        if (gl == 0) {
-            {
-                double d[NX];
-#pragma unroll
-                for (int r = 0; r < NX; ++r) {
-                    d[r] = 0.0;
-                    sD[r] = 0.0;
-                }
-                for (int k = 0; k < N; ++k) {
-                    double dn[NX];
-                    a_mul<NQ, double>(h, sFq + k * NQ * NQ, sFqd + k * NQ * NQ, d, dn);
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) {
-                        d[r] = dn[r] + sC[k * NX + r];
-                        sD[(k + 1) * NX + r] = d[r];
-                    }
-                }
-            }
+        const double beps = BOUNDED ? fmin(kBoundEps, pg_prev) : 0.0;
+        // backward sweep of QP solve `pass` (gradient and stop-test quantities are the same in every pass)
+        auto backward = [&](int pass) {
             // P~ (symmetric, upper triangle used) and p~ on s = [dx_k; du_{k-1}]; P~_N = blkdiag(Q, 0)
             double P[NS][NS], pv[NS], lam[NX], unext[NU];
 #define Ps(i, j) ((i) <= (j) ? P[(i)][(j)] : P[(j)][(i)])
@@ -250,7 +239,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             for (int k = N - 1; k >= 0; --k) {
                 const double* hFq = sFq + k * NQ * NQ;
                 const double* hFqd = sFqd + k * NQ * NQ;
-                double hFu[NQ * NU], x[NX], u[NU], um[NU], cc[NX];
+                double hFu[NQ * NU], x[NX], u[NU], um[NU], cc[NX], tg[NU];
 #pragma unroll
                 for (int i = 0; i < NQ * NU; ++i) hFu[i] = sFu[k * NQ * NU + i];
 #pragma unroll
@@ -271,7 +260,19 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     for (int s = 0; s < NQ; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
                     g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
                     if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
-                    gmax = fmax(gmax, fabs(2.0 * g));
+                    if (!BOUNDED) {
+                        gmax = fmax(gmax, fabs(2.0 * g));
+                    } else {  // projected gradient; hold rule (pass 0) or the holds of the previous solve
+                        gmax = fmax(gmax, fabs(u[c] - proj(u[c] - 2.0 * g, lbv[c], ubv[c])));
+                        if (pass == 0) {
+                            tg[c] = (u[c] <= lbv[c] + beps && g > 0.0)   ? lbv[c]
+                                    : (u[c] >= ubv[c] - beps && g < 0.0) ? ubv[c]
+                                                                          : NAN;
+                            sHold[k * NU + c] = tg[c];
+                        } else {
+                            tg[c] = sHold[k * NU + c];
+                        }
+                    }
                     nonfinite |= !isfinite(g);
                     unext[c] = u[c];
                 }
@@ -328,6 +329,42 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     at_mul<NQ, double>(h, hFq, hFqd, ga, &Y[a][0]);
 #pragma unroll
                     for (int c = 0; c < NU; ++c) Y[a][NX + c] = (a == c) ? -R[a] : 0.0;
+                }
+                // held controls (bounded): w_A = target - u fixed in the stage QP, as sqp_lane.h
+                double pex[NS];
+                if (BOUNDED) {
+                    bool hd[NU], any = false;
+                    double dl[NU];
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) pex[j] = 0.0;
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        hd[a] = tg[a] == tg[a];
+                        dl[a] = hd[a] ? tg[a] - u[a] : 0.0;
+                        any |= hd[a];
+                    }
+                    if (any) {
+#pragma unroll
+                        for (int a = 0; a < NU; ++a)
+#pragma unroll
+                            for (int j = 0; j < NS; ++j) pex[j] = fma(Y[a][j], dl[a], pex[j]);
+#pragma unroll
+                        for (int b = 0; b < NU; ++b) {
+                            double t = Y[b][NS];
+#pragma unroll
+                            for (int a = 0; a < NU; ++a) t = fma(Hww[a < b ? a : b][a < b ? b : a], dl[a], t);
+                            Y[b][NS] = hd[b] ? -dl[b] : t;
+                        }
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) {
+#pragma unroll
+                            for (int b = a; b < NU; ++b)
+                                if (hd[a] || hd[b]) Hww[a][b] = (a == b) ? 1.0 : 0.0;
+                            if (hd[a])
+#pragma unroll
+                                for (int j = 0; j < NS; ++j) Y[a][j] = 0.0;
+                        }
+                    }
                 }
                 // P~_k x block A^T P_xx A + Q and p~_k x part A^T mv + Q (x_k - r_{k-1}), before P is overwritten
                 double Pn[NX][NX], pn[NS];
@@ -409,6 +446,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     double t = pn[a];
 #pragma unroll
                     for (int q = 0; q < NU; ++q) t = fma(-Y[q][a], Y[q][NS], t);
+                    if (BOUNDED) t += pex[a];
                     pv[a] = t;
 #pragma unroll
                     for (int b = a; b < NS; ++b) {
@@ -420,42 +458,12 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 }
             }
 #undef Ps
-        }
-        gmax = group_bcast(gmax, gbase);
-        lmax = group_bcast(lmax, gbase);
-        fact_ok = group_bcast_i(fact_ok, gbase);
-        MMPC_PHASE(2);
-        nonfinite = (group_max((double)nonfinite) != 0.0);
-        kkt = fmax(gmax, cmax);
-        double* trc = p.trace && valid ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
-        if (trc && gl == 0) {
-            trc[0] = gmax;
-            trc[1] = cmax;
-            trc[2] = J0;
-            trc[3] = c1;
-            trc[7] = lmax;
-        }
-        if (nonfinite || !isfinite(kkt)) {
-            status = ST_NONFINITE;
-            break;
-        }
-        if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
-            status = ST_CONVERGED;
-            break;
-        }
-        if (it == p.max_iter) {
-            status = ST_MAX_ITER;
-            break;
-        }
-        if (!fact_ok) {
-            status = ST_FACT_FAILED;
-            break;
-        }
-
-        MMPC_PHASE(3);
+        };
         // ---- C. one lane: step sweep du = K s + kff, dx, directional derivative ----
         double dJ = 0.0;
-        if (gl == 0) {
+        bool resolve = false;
+        auto step_sweep = [&](int pass) {
+            dJ = 0.0;
             double dx[NX], dup[NU], um[NU];
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
@@ -471,21 +479,21 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             constexpr int NK = NU * (NS + 1);
             double nK[NK], nFq[NQ * NQ], nFqd[NQ * NQ], nFu[NQ * NU], nF[NX], nc[NX], nr[NX], nu_[NU];
 #define GROUP_LOAD_STEP(k_)                                                                        \
-    do {                                                                                           \
-        const int kk_ = (k_);                                                                      \
-        _Pragma("unroll") for (int i_ = 0; i_ < NK; ++i_) nK[i_] = wK[kk_ * NK + i_];              \
-        _Pragma("unroll") for (int i_ = 0; i_ < NQ * NQ; ++i_) {                                   \
+        do {                                                                                           \
+            const int kk_ = (k_);                                                                      \
+            _Pragma("unroll") for (int i_ = 0; i_ < NK; ++i_) nK[i_] = wK[kk_ * NK + i_];              \
+            _Pragma("unroll") for (int i_ = 0; i_ < NQ * NQ; ++i_) {                                   \
             nFq[i_] = sFq[kk_ * NQ * NQ + i_];                                                     \
             nFqd[i_] = sFqd[kk_ * NQ * NQ + i_];                                                   \
-        }                                                                                          \
-        _Pragma("unroll") for (int i_ = 0; i_ < NQ * NU; ++i_) nFu[i_] = sFu[kk_ * NQ * NU + i_];  \
-        _Pragma("unroll") for (int r_ = 0; r_ < NX; ++r_) {                                        \
+            }                                                                                          \
+            _Pragma("unroll") for (int i_ = 0; i_ < NQ * NU; ++i_) nFu[i_] = sFu[kk_ * NQ * NU + i_];  \
+            _Pragma("unroll") for (int r_ = 0; r_ < NX; ++r_) {                                        \
             nF[r_] = sF[kk_ * NX + r_];                                                            \
             nc[r_] = sC[kk_ * NX + r_];                                                            \
             nr[r_] = sR[kk_ * NX + r_];                                                            \
-        }                                                                                          \
-        _Pragma("unroll") for (int c_ = 0; c_ < NU; ++c_) nu_[c_] = sU[kk_ * NU + c_];             \
-    } while (0)
+            }                                                                                          \
+            _Pragma("unroll") for (int c_ = 0; c_ < NU; ++c_) nu_[c_] = sU[kk_ * NU + c_];             \
+        } while (0)
             GROUP_LOAD_STEP(0);
             for (int k = 0; k < N; ++k) {
                 double K[NK], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU], Fk[NX], ck[NX], rk[NX], uk[NU];
@@ -518,6 +526,16 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     du[a] = t;
                     sDU[k * NU + a] = t;
                 }
+                if (BOUNDED && pass + 1 < kBoundPasses) {  // a free control whose step crosses a bound: hold it
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        const double hv = sHold[k * NU + a], t = uk[a] + du[a];
+                        if (hv != hv && (t < lbv[a] || t > ubv[a])) {
+                            sHold[k * NU + a] = t < lbv[a] ? lbv[a] : ubv[a];
+                            resolve = true;
+                        }
+                    }
+                }
                 double ad[NX];
                 a_mul<NQ, double>(h, hFq, hFqd, dx, ad);
 #pragma unroll
@@ -540,6 +558,73 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 }
             }
 #undef GROUP_LOAD_STEP
+        };
+        if (gl == 0) {
+            {
+                double d[NX];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    d[r] = 0.0;
+                    sD[r] = 0.0;
+                }
+                for (int k = 0; k < N; ++k) {
+                    double dn[NX];
+                    a_mul<NQ, double>(h, sFq + k * NQ * NQ, sFqd + k * NQ * NQ, d, dn);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        d[r] = dn[r] + sC[k * NX + r];
+                        sD[(k + 1) * NX + r] = d[r];
+                    }
+                }
+            }
+            backward(0);
+        }
+        gmax = group_bcast(gmax, gbase);
+        lmax = group_bcast(lmax, gbase);
+        fact_ok = group_bcast_i(fact_ok, gbase);
+        MMPC_PHASE(2);
+        nonfinite = (group_max((double)nonfinite) != 0.0);
+        kkt = fmax(gmax, cmax);
+        double* trc = p.trace && valid ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
+        if (trc && gl == 0) {
+            trc[0] = gmax;
+            trc[1] = cmax;
+            trc[2] = J0;
+            trc[3] = c1;
+            trc[7] = lmax;
+        }
+        if (nonfinite || !isfinite(kkt)) {
+            status = ST_NONFINITE;
+            break;
+        }
+        if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
+            status = ST_CONVERGED;
+            break;
+        }
+        if (it == p.max_iter) {
+            status = ST_MAX_ITER;
+            break;
+        }
+        if (!fact_ok) {
+            status = ST_FACT_FAILED;
+            break;
+        }
+        if (BOUNDED) pg_prev = gmax;
+
+        MMPC_PHASE(3);
+        if (gl == 0) {
+            for (int pass = 0;; ++pass) {
+                if (pass > 0) backward(pass);
+                if (!fact_ok) break;
+                resolve = false;
+                step_sweep(pass);
+                if (!BOUNDED || !resolve || pass + 1 >= kBoundPasses) break;
+            }
+        }
+        fact_ok = group_bcast_i(fact_ok, gbase);
+        if (!fact_ok) {
+            status = ST_FACT_FAILED;
+            break;
         }
         dJ = group_bcast(dJ, gbase);
         __builtin_amdgcn_wave_barrier();
@@ -558,7 +643,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                 for (int r = 0; r < NX; ++r) x[r] = fma(alpha, sDX[k * NX + r], sX[k * NX + r]);
 #pragma unroll
-                for (int c = 0; c < NU; ++c) u[c] = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
+                for (int c = 0; c < NU; ++c) {
+                    u[c] = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
+                    if (BOUNDED) u[c] = proj(u[c], lbv[c], ubv[c]);  // projected trial point
+                }
                 group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, nullptr, nullptr, nullptr, false);
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
@@ -569,8 +657,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 }
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
-                    const double um =
-                        (k == 0) ? up[c] : fma(alpha, sDU[(k - 1) * NU + c], sU[(k - 1) * NU + c]);
+                    double um = (k == 0) ? up[c] : fma(alpha, sDU[(k - 1) * NU + c], sU[(k - 1) * NU + c]);
+                    if (BOUNDED && k > 0) um = proj(um, lbv[c], ubv[c]);
                     const double dif = u[c] - um;
                     Jt = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], Jt));
                 }
@@ -603,25 +691,16 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             }
             if (k < N) {
 #pragma unroll
-                for (int c = 0; c < NU; ++c) sU[k * NU + c] = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
+                for (int c = 0; c < NU; ++c) {
+                    const double un = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
+                    sU[k * NU + c] = BOUNDED ? proj(un, lbv[c], ubv[c]) : un;
+                }
             }
         }
     }
     __builtin_amdgcn_wave_barrier();
     MMPC_PHASE(6);
     if (!valid) return;
-    // ---- bounds check (reported, not enforced), as sqp_wave.h ----
-    if (status == ST_CONVERGED && (p.u_lb || p.u_ub)) {
-        bool viol = false;
-        for (int k = gl; k < N; k += G)
-#pragma unroll
-            for (int r = 0; r < NU; ++r) {
-                const double u = sU[k * NU + r];
-                if (p.u_lb) viol |= (p.u_lb[r] > -1e19) && (u < p.u_lb[r] - 1e-9);
-                if (p.u_ub) viol |= (p.u_ub[r] < 1e19) && (u > p.u_ub[r] + 1e-9);
-            }
-        if (group_max(viol ? 1.0 : 0.0) != 0.0) status = ST_BOUNDS;
-    }
     // ---- write back V (reference layout), stage-parallel ----
     double* Vout = p.V + inst * (int64_t)NV;
     for (int k = gl; k <= N; k += G) {

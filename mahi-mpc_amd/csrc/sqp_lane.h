@@ -32,7 +32,7 @@ namespace mmpc {
 // scalar registers plus the lane offset in one VGPR (an [element][lane] layout hoists one 64-bit
 // per-lane pointer per (field, element) and spills).  Stage N holds x_N, d_N, dx_N; stage N+1 holds
 // the linear-mode data; stage N+2 is per-lane scratch for the Riccati step (W = P_xx A).
-__host__ __device__ constexpr int lane_stage_stride(int nx, int nu) { return 5 * nx + 2 * nu + nu * (nx + nu + 1); }
+__host__ __device__ constexpr int lane_stage_stride(int nx, int nu) { return 5 * nx + 3 * nu + nu * (nx + nu + 1); }
 __host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int N) { return (N + 3) * lane_stage_stride(nx, nu); }
 template <int NX, int NU>
 struct StageFields {
@@ -45,7 +45,8 @@ struct StageFields {
     static constexpr int DX = D + NX;       // dx_k
     static constexpr int DU = DX + NX;      // du_k
     static constexpr int K = DU + NU;       // kff_k (nu, fp64) then K_k (nu x (nx+nu), factor type)
-    static constexpr int SS = K + NU * (NS + 1);
+    static constexpr int HOLD = K + NU * (NS + 1);  // bounded solves: bound u_k is held at, NaN = free
+    static constexpr int SS = HOLD + NU;
     static_assert(SS == lane_stage_stride(NX, NU), "layout");
     static_assert(NX * NX <= SS, "Riccati scratch W fits one stage");
 };
@@ -101,7 +102,7 @@ __device__ __forceinline__ double* stage_ptr(double* wsb, int64_t k, int SS, int
 // FT: arithmetic type of the Riccati factor/solve (double, or float for SURVEY.md 8d cfg#5: the backward
 // recursion, P in LDS, the gains K and the W scratch in fp32; model evaluations, defects, adjoint, gradient,
 // merit and iterates stay fp64, so every SQP iteration refines the fp32 step against fp64 residuals).
-template <class Model, class FT = double>
+template <class Model, class FT = double, bool BOUNDED = false>
 __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw) {
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NS = NX + NU, ND = NX + NU;
     static_assert(NX == 2 * NQ, "second-order models only (x = [q; qd])");
@@ -134,6 +135,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         Rm[c] = w[NX + NU + c];
         up[c] = p.u_prev[inst * NU + c];
     }
+    double lbv[NU], ubv[NU];
+    load_bounds<NU, BOUNDED>(p, lbv, ubv);
     // ---- load: V (reference layout) -> SoA X/U, x_0 pinned (ModelControl.cpp:144-145), targets ----
     {
         const double* Vin = p.V + inst * (int64_t)NV;
@@ -141,7 +144,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
 #pragma unroll
             for (int r = 0; r < NX; ++r) ST(k, SF::X, r) = (k == 0) ? p.x0[inst * NX + r] : Vin[k * ND + r];
 #pragma unroll
-            for (int c = 0; c < NU; ++c) ST(k, SF::U, c) = Vin[k * ND + NX + c];
+            for (int c = 0; c < NU; ++c)
+                ST(k, SF::U, c) = BOUNDED ? proj(Vin[k * ND + NX + c], lbv[c], ubv[c]) : Vin[k * ND + NX + c];
         }
 #pragma unroll
         for (int r = 0; r < NX; ++r) ST(N, SF::X, r) = Vin[N * ND + r];
@@ -223,7 +227,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
 
     int status = ST_MAX_ITER;
     int it = 0;
-    double kkt = 0.0, mu = 0.0;
+    double kkt = 0.0, mu = 0.0, pg_prev = INFINITY;
     MMPC_PHASE(0);
     #pragma unroll 1
     for (it = 0; it <= p.max_iter; ++it) {
@@ -286,366 +290,445 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         }
 
         MMPC_PHASE(1);
-        // ---- (2) backward: adjoint + reduced gradient (stopping test) and the Riccati recursion ----
-        // Value function V_k(s) = s^T P s + 2 p^T s on s = [dx_k; du_{k-1}] (no 1/2: J has none,
-        // ModelGenerator.cpp:208-222); (P, pv) hold P~_{k+1} = P_{k+1} + blkdiag(Q, 0) on entry to step k.
-        double gmax = 0.0, lmax = 0.0;
-        bool fact_ok = true;
-        {
-            double pv[NS], lam[NX], unext[NU];
+        // (2)+(3) run once, or (bounded) again after holding controls whose step crosses a bound
+        double gmax = 0.0, lmax = 0.0, dJ = 0.0;
+        bool fact_ok = true, done = false;
+        const double beps = BOUNDED ? fmin(kBoundEps, pg_prev) : 0.0;
+        // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
+        double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
+        #pragma unroll 1
+        for (int pass = 0;; ++pass) {
+            bool resolve = false;
+            gmax = 0.0;
+            lmax = 0.0;
+            fact_ok = true;
+            // ---- (2) backward: adjoint + reduced gradient (stopping test) and the Riccati recursion ----
+            // Value function V_k(s) = s^T P s + 2 p^T s on s = [dx_k; du_{k-1}] (no 1/2: J has none,
+            // ModelGenerator.cpp:208-222); (P, pv) hold P~_{k+1} = P_{k+1} + blkdiag(Q, 0) on entry to step k.
+            {
+                double pv[NS], lam[NX], unext[NU];
 #pragma unroll
-            for (int a = 0; a < NS; ++a) {
-                pv[a] = 0.0;
+                for (int a = 0; a < NS; ++a) {
+                    pv[a] = 0.0;
 #pragma unroll
-                for (int b = a; b < NS; ++b) PS(a, b) = (FT)((a == b && a < NX) ? Q[a] : 0.0);
-            }
-#pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                const double eb = ST(N, SF::X, r) - ST(N - 1, SF::R, r);  // x_N - r_{N-1}
-                pv[r] = Q[r] * eb;
-                lam[r] = Q[r] * (ST(N, SF::D, r) + eb);  // lam_N = Q e_{N-1}
-                lmax = fmax(lmax, fabs(lam[r]));
-            }
-            // software pipeline as in (1): x_{k-1}, u_{k-1} (model inputs of the next step) are loaded during
-            // step k, everything else of step k before its model evaluation
-            double xpf[NX], upf[NU];
-#pragma unroll
-            for (int c = 0; c < NU; ++c) {
-                unext[c] = 0.0;
-                upf[c] = ST(N - 1, SF::U, c);
-            }
-#pragma unroll
-            for (int r = 0; r < NX; ++r) xpf[r] = ST(N - 1, SF::X, r);
-            #pragma unroll 1
-            for (int k = N - 1; k >= 0; --k) {
-                double* const sk = stage_ptr(wsb, k, SS, lane);
-                double x[NX], u[NU], um[NU], cc[NX], dk[NX], rkm[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ],
-                    hFu[NQ * NU];
+                    for (int b = a; b < NS; ++b) PS(a, b) = (FT)((a == b && a < NX) ? Q[a] : 0.0);
+                }
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
-                    x[r] = xpf[r];
-                    cc[r] = SK(0, SF::C, r);
-                    dk[r] = SK(0, SF::D, r);
+                    const double eb = ST(N, SF::X, r) - ST(N - 1, SF::R, r);  // x_N - r_{N-1}
+                    pv[r] = Q[r] * eb;
+                    lam[r] = Q[r] * (ST(N, SF::D, r) + eb);  // lam_N = Q e_{N-1}
+                    lmax = fmax(lmax, fabs(lam[r]));
                 }
-#pragma unroll
-                for (int c = 0; c < NU; ++c) u[c] = upf[c];
-                if (k >= 1) {
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) {
-                        rkm[r] = SK(-1, SF::R, r);
-                        xpf[r] = SK(-1, SF::X, r);
-                    }
-#pragma unroll
-                    for (int c = 0; c < NU; ++c) um[c] = SK(-1, SF::U, c);
-                } else {
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) rkm[r] = 0.0;
-#pragma unroll
-                    for (int c = 0; c < NU; ++c) um[c] = up[c];
-                }
-#pragma unroll
-                for (int c = 0; c < NU; ++c) upf[c] = um[c];
-                STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
-                // reduced gradient g_k = B_k^T lam_{k+1} + R/Rm terms (same expression as sqp_wave.h)
+                // software pipeline as in (1): x_{k-1}, u_{k-1} (model inputs of the next step) are loaded during
+                // step k, everything else of step k before its model evaluation
+                double xpf[NX], upf[NU];
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
-                    double g = 0.0;
-#pragma unroll
-                    for (int s = 0; s < NQ; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
-                    g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
-                    if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
-                    gmax = fmax(gmax, fabs(2.0 * g));
-                    nonfinite |= !isfinite(g);
-                    unext[c] = u[c];
+                    unext[c] = 0.0;
+                    upf[c] = ST(N - 1, SF::U, c);
                 }
-                // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1},  e_{k-1} = d_k + x_k - r_{k-1}
-                if (k >= 1) {
-                    double ln[NX];
-                    at_mul<NQ>(h, hFq, hFqd, lam, ln);
+#pragma unroll
+                for (int r = 0; r < NX; ++r) xpf[r] = ST(N - 1, SF::X, r);
+                #pragma unroll 1
+                for (int k = N - 1; k >= 0; --k) {
+                    double* const sk = stage_ptr(wsb, k, SS, lane);
+                    double x[NX], u[NU], um[NU], cc[NX], dk[NX], rkm[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ],
+                        hFu[NQ * NU], tg[NU];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
-                        lam[r] = fma(Q[r], dk[r] + x[r] - rkm[r], ln[r]);
-                        lmax = fmax(lmax, fabs(lam[r]));
+                        x[r] = xpf[r];
+                        cc[r] = SK(0, SF::C, r);
+                        dk[r] = SK(0, SF::D, r);
                     }
-                }
-                // ---- Riccati step ----
-                // Matrix recursion (P, G, H_ww, its Cholesky factor, the matrix part of Y and K) in FT; the
-                // right-hand side (p, m = P_xx c + p_x, h_w, y, kff) in fp64 with FT matrices: with FT = float
-                // this is an fp32 factorisation applied to fp64 residuals, so each SQP iteration is a
-                // refinement step (the linear terms cancel down to the gradient and need fp64).
-                FT fq[NQ * NQ], fqd[NQ * NQ], fu[NQ * NU];
-                const FT hf = (FT)h;
 #pragma unroll
-                for (int i = 0; i < NQ * NQ; ++i) {
-                    fq[i] = (FT)hFq[i];
-                    fqd[i] = (FT)hFqd[i];
-                }
+                    for (int c = 0; c < NU; ++c) u[c] = upf[c];
+                    if (k >= 1) {
 #pragma unroll
-                for (int i = 0; i < NQ * NU; ++i) fu[i] = (FT)hFu[i];
-                FT G[NX][NU];  // P_xx B + P_xu   (B = [0; hFu])
+                        for (int r = 0; r < NX; ++r) {
+                            rkm[r] = SK(-1, SF::R, r);
+                            xpf[r] = SK(-1, SF::X, r);
+                        }
 #pragma unroll
-                for (int r = 0; r < NX; ++r)
+                        for (int c = 0; c < NU; ++c) um[c] = SK(-1, SF::U, c);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) rkm[r] = 0.0;
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) um[c] = up[c];
+                    }
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) upf[c] = um[c];
+                    STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                    // reduced gradient g_k = B_k^T lam_{k+1} + R/Rm terms (same expression as sqp_wave.h)
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
-                        FT t = PS(r, NX + c);
+                        double g = 0.0;
 #pragma unroll
-                        for (int s = 0; s < NQ; ++s) t = fma(PS(r, NQ + s), fu[s * NU + c], t);
-                        G[r][c] = t;
+                        for (int s = 0; s < NQ; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
+                        g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
+                        if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
+                        if (!BOUNDED) {
+                            gmax = fmax(gmax, fabs(2.0 * g));
+                        } else {  // projected gradient; hold rule (pass 0) or the holds of the previous solve
+                            gmax = fmax(gmax, fabs(u[c] - proj(u[c] - 2.0 * g, lbv[c], ubv[c])));
+                            if (pass == 0) {
+                                tg[c] = (u[c] <= lbv[c] + beps && g > 0.0)   ? lbv[c]
+                                        : (u[c] >= ubv[c] - beps && g < 0.0) ? ubv[c]
+                                                                              : NAN;
+                                SK(0, SF::HOLD, c) = tg[c];
+                            } else {
+                                tg[c] = SK(0, SF::HOLD, c);
+                            }
+                        }
+                        nonfinite |= !isfinite(g);
+                        unext[c] = u[c];
                     }
-                double mv[NX];  // P_xx c + p_x (fp64)
+                    // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1},  e_{k-1} = d_k + x_k - r_{k-1}
+                    if (k >= 1) {
+                        double ln[NX];
+                        at_mul<NQ>(h, hFq, hFqd, lam, ln);
 #pragma unroll
-                for (int r = 0; r < NX; ++r) {
-                    double t = pv[r];
-#pragma unroll
-                    for (int q = 0; q < NX; ++q) t = fma((double)PS(r, q), cc[q], t);
-                    mv[r] = t;
-                }
-                FT Hww[NU][NU], Y[NU][NS];  // Y rows: L^-1 [H_wx | -R]
-                double yh[NU];              // L^-1 h_w (fp64)
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-#pragma unroll
-                    for (int b = a; b < NU; ++b) {
-                        FT t = PS(NX + a, NX + b);
-#pragma unroll
-                        for (int s = 0; s < NQ; ++s)
-                            t = fma(fu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), fu[s * NU + b], t));
-                        if (a == b) t += (FT)(R[a] + Rm[a]);
-                        Hww[a][b] = t;
+                        for (int r = 0; r < NX; ++r) {
+                            lam[r] = fma(Q[r], dk[r] + x[r] - rkm[r], ln[r]);
+                            lmax = fmax(lmax, fabs(lam[r]));
+                        }
                     }
-                    double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
+                    // ---- Riccati step ----
+                    // Matrix recursion (P, G, H_ww, its Cholesky factor, the matrix part of Y and K) in FT; the
+                    // right-hand side (p, m = P_xx c + p_x, h_w, y, kff) in fp64 with FT matrices: with FT = float
+                    // this is an fp32 factorisation applied to fp64 residuals, so each SQP iteration is a
+                    // refinement step (the linear terms cancel down to the gradient and need fp64).
+                    FT fq[NQ * NQ], fqd[NQ * NQ], fu[NQ * NU];
+                    const FT hf = (FT)h;
 #pragma unroll
-                    for (int s = 0; s < NQ; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
+                    for (int i = 0; i < NQ * NQ; ++i) {
+                        fq[i] = (FT)hFq[i];
+                        fqd[i] = (FT)hFqd[i];
+                    }
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) t = fma((double)PS(r, NX + a), cc[r], t);
-                    yh[a] = t;
-                    FT ga[NX];
+                    for (int i = 0; i < NQ * NU; ++i) fu[i] = (FT)hFu[i];
+                    FT G[NX][NU];  // P_xx B + P_xu   (B = [0; hFu])
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) ga[r] = G[r][a];
-                    at_mul<NQ, FT>(hf, fq, fqd, ga, &Y[a][0]);  // H_wx row a = (A^T G[:, a])^T
+                    for (int r = 0; r < NX; ++r)
 #pragma unroll
-                    for (int c = 0; c < NU; ++c) Y[a][NX + c] = (FT)((a == c) ? -R[a] : 0.0);
-                }
-                // W = P_xx A (row r of W = (A^T P_xx[r][:])^T), streamed through the lane's scratch stage of the
-                // workspace (in registers next to G, Y and the stage blocks it spills).
-                // p~_k x part: A^T mv + Q (x_k - r_{k-1}) (fp64).
-                double pn[NS];
-                FT* const sw = reinterpret_cast<FT*>(stage_ptr(wsb, N + 2, SS, 0)) + lane;  // per-lane scratch stage
-                if (k >= 1) {
+                        for (int c = 0; c < NU; ++c) {
+                            FT t = PS(r, NX + c);
+#pragma unroll
+                            for (int s = 0; s < NQ; ++s) t = fma(PS(r, NQ + s), fu[s * NU + c], t);
+                            G[r][c] = t;
+                        }
+                    double mv[NX];  // P_xx c + p_x (fp64)
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
-                        FT prow[NX], wrow[NX];
+                        double t = pv[r];
 #pragma unroll
-                        for (int q = 0; q < NX; ++q) prow[q] = PS(r, q);
-                        at_mul<NQ, FT>(hf, fq, fqd, prow, wrow);
-#pragma unroll
-                        for (int b = 0; b < NX; ++b) sw[(r * NX + b) * 64] = wrow[b];
+                        for (int q = 0; q < NX; ++q) t = fma((double)PS(r, q), cc[q], t);
+                        mv[r] = t;
                     }
-                    double t[NX];
-                    at_mul<NQ, double>(h, hFq, hFqd, mv, t);
+                    FT Hww[NU][NU], Y[NU][NS];  // Y rows: L^-1 [H_wx | -R]
+                    double yh[NU];              // L^-1 h_w (fp64)
 #pragma unroll
-                    for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - rkm[q], t[q]);
+                    for (int a = 0; a < NU; ++a) {
 #pragma unroll
-                    for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
-                }
-                // Cholesky H_ww = L L^T (FT), then Y <- L^-1 Y (FT) and yh <- L^-1 yh (fp64)
-                FT Ld[NU][NU], il[NU];
+                        for (int b = a; b < NU; ++b) {
+                            FT t = PS(NX + a, NX + b);
 #pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    FT s = Hww[a][a];
+                            for (int s = 0; s < NQ; ++s)
+                                t = fma(fu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), fu[s * NU + b], t));
+                            if (a == b) t += (FT)(R[a] + Rm[a]);
+                            Hww[a][b] = t;
+                        }
+                        double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
 #pragma unroll
-                    for (int q = 0; q < a; ++q) s = fma(-Ld[a][q], Ld[a][q], s);
-                    fact_ok &= (s > (FT)0) && isfinite(s);
-                    const FT lj = sqrt(fmax(s, std::numeric_limits<FT>::min()));
-                    Ld[a][a] = lj;
-                    il[a] = (FT)1 / lj;
+                        for (int s = 0; s < NQ; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
 #pragma unroll
-                    for (int b = a + 1; b < NU; ++b) {
-                        FT t = Hww[a][b];
+                        for (int r = 0; r < NX; ++r) t = fma((double)PS(r, NX + a), cc[r], t);
+                        yh[a] = t;
+                        FT ga[NX];
 #pragma unroll
-                        for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
-                        Ld[b][a] = t * il[a];
+                        for (int r = 0; r < NX; ++r) ga[r] = G[r][a];
+                        at_mul<NQ, FT>(hf, fq, fqd, ga, &Y[a][0]);  // H_wx row a = (A^T G[:, a])^T
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) Y[a][NX + c] = (FT)((a == c) ? -R[a] : 0.0);
                     }
-                }
+                    // Held controls (bounded solves): the stage QP with w_A = delta_A = target - u fixed --
+                    // h_F += H_FA delta_A, rows/cols A of H_ww -> identity, rows A of [H_wx | -R] -> 0, so that
+                    // K_A = 0 and kff_A = delta_A; p~_k gains [H_wx | -R]_A^T delta_A (pex).
+                    double pex[NS];
+                    if (BOUNDED) {
+                        bool hd[NU], any = false;
+                        double dl[NU];
 #pragma unroll
-                for (int a = 0; a < NU; ++a) {
+                        for (int j = 0; j < NS; ++j) pex[j] = 0.0;
 #pragma unroll
-                    for (int j = 0; j < NS; ++j) {
-                        FT t = Y[a][j];
+                        for (int a = 0; a < NU; ++a) {
+                            hd[a] = tg[a] == tg[a];
+                            dl[a] = hd[a] ? tg[a] - u[a] : 0.0;
+                            any |= hd[a];
+                        }
+                        if (any) {
 #pragma unroll
-                        for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
-                        Y[a][j] = t * il[a];
+                            for (int a = 0; a < NU; ++a)
+#pragma unroll
+                                for (int j = 0; j < NS; ++j) pex[j] = fma((double)Y[a][j], dl[a], pex[j]);
+#pragma unroll
+                            for (int b = 0; b < NU; ++b) {
+                                double t = yh[b];
+#pragma unroll
+                                for (int a = 0; a < NU; ++a) t = fma((double)Hww[a < b ? a : b][a < b ? b : a], dl[a], t);
+                                yh[b] = hd[b] ? -dl[b] : t;
+                            }
+#pragma unroll
+                            for (int a = 0; a < NU; ++a) {
+#pragma unroll
+                                for (int b = a; b < NU; ++b)
+                                    if (hd[a] || hd[b]) Hww[a][b] = (FT)((a == b) ? 1.0 : 0.0);
+                                if (hd[a])
+#pragma unroll
+                                    for (int j = 0; j < NS; ++j) Y[a][j] = (FT)0;
+                            }
+                        }
                     }
-                    double t = yh[a];
+                    // W = P_xx A (row r of W = (A^T P_xx[r][:])^T), streamed through the lane's scratch stage of the
+                    // workspace (in registers next to G, Y and the stage blocks it spills).
+                    // p~_k x part: A^T mv + Q (x_k - r_{k-1}) (fp64).
+                    double pn[NS];
+                    FT* const sw = reinterpret_cast<FT*>(stage_ptr(wsb, N + 2, SS, 0)) + lane;  // per-lane scratch stage
+                    if (k >= 1) {
 #pragma unroll
-                    for (int q = 0; q < a; ++q) t = fma(-(double)Ld[a][q], yh[q], t);
-                    yh[a] = t / (double)Ld[a][a];
-                }
-                // [K_k | kff_k] = -L^-T [Y | yh]: kff (fp64) in the first NU slots of the K field, K (FT) after it
-                {
-                    FT Kt[NU][NS];
-                    double kh[NU];
+                        for (int r = 0; r < NX; ++r) {
+                            FT prow[NX], wrow[NX];
 #pragma unroll
-                    for (int a = NU - 1; a >= 0; --a) {
+                            for (int q = 0; q < NX; ++q) prow[q] = PS(r, q);
+                            at_mul<NQ, FT>(hf, fq, fqd, prow, wrow);
+#pragma unroll
+                            for (int b = 0; b < NX; ++b) sw[(r * NX + b) * 64] = wrow[b];
+                        }
+                        double t[NX];
+                        at_mul<NQ, double>(h, hFq, hFqd, mv, t);
+#pragma unroll
+                        for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - rkm[q], t[q]);
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
+                    }
+                    // Cholesky H_ww = L L^T (FT), then Y <- L^-1 Y (FT) and yh <- L^-1 yh (fp64)
+                    FT Ld[NU][NU], il[NU];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        FT s = Hww[a][a];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) s = fma(-Ld[a][q], Ld[a][q], s);
+                        fact_ok &= (s > (FT)0) && isfinite(s);
+                        const FT lj = sqrt(fmax(s, std::numeric_limits<FT>::min()));
+                        Ld[a][a] = lj;
+                        il[a] = (FT)1 / lj;
+#pragma unroll
+                        for (int b = a + 1; b < NU; ++b) {
+                            FT t = Hww[a][b];
+#pragma unroll
+                            for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
+                            Ld[b][a] = t * il[a];
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
 #pragma unroll
                         for (int j = 0; j < NS; ++j) {
                             FT t = Y[a][j];
 #pragma unroll
-                            for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], Kt[q][j], t);
-                            Kt[a][j] = t * il[a];
+                            for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
+                            Y[a][j] = t * il[a];
                         }
                         double t = yh[a];
 #pragma unroll
-                        for (int q = a + 1; q < NU; ++q) t = fma(-(double)Ld[q][a], kh[q], t);
-                        kh[a] = t / (double)Ld[a][a];
+                        for (int q = 0; q < a; ++q) t = fma(-(double)Ld[a][q], yh[q], t);
+                        yh[a] = t / (double)Ld[a][a];
                     }
-                    double* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
-                    FT* const kk = reinterpret_cast<FT*>(kb + NU * 64) + lane;
+                    // [K_k | kff_k] = -L^-T [Y | yh]: kff (fp64) in the first NU slots of the K field, K (FT) after it
+                    {
+                        FT Kt[NU][NS];
+                        double kh[NU];
+#pragma unroll
+                        for (int a = NU - 1; a >= 0; --a) {
+#pragma unroll
+                            for (int j = 0; j < NS; ++j) {
+                                FT t = Y[a][j];
+#pragma unroll
+                                for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], Kt[q][j], t);
+                                Kt[a][j] = t * il[a];
+                            }
+                            double t = yh[a];
+#pragma unroll
+                            for (int q = a + 1; q < NU; ++q) t = fma(-(double)Ld[q][a], kh[q], t);
+                            kh[a] = t / (double)Ld[a][a];
+                        }
+                        double* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
+                        FT* const kk = reinterpret_cast<FT*>(kb + NU * 64) + lane;
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) {
+                            kb[a * 64 + lane] = -kh[a];
+#pragma unroll
+                            for (int j = 0; j < NS; ++j) kk[(a * NS + j) * 64] = -Kt[a][j];
+                        }
+                    }
+                    if (k == 0) break;  // s_0 = 0: P~_0 is never used
+                    // P~_k = blkdiag(A^T W + Q, R) - Y^T Y (old P is dead: overwrite it in place), p~_k = pn - Y^T yh
+                    asm volatile("" ::: "memory");  // W comes back from memory, not from forwarded registers
+#pragma unroll
+                    for (int b = 0; b < NX; ++b) {
+                        FT wcol[NX], col[NX];
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) wcol[r] = sw[(r * NX + b) * 64];
+                        at_mul<NQ, FT>(hf, fq, fqd, wcol, col);
+#pragma unroll
+                        for (int a = 0; a <= b; ++a) {
+                            FT v = col[a] + (FT)((a == b) ? Q[a] : 0.0);
+#pragma unroll
+                            for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
+                            PS(a, b) = v;
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < NS; ++a) {
+                        double t = pn[a];
+#pragma unroll
+                        for (int q = 0; q < NU; ++q) t = fma(-(double)Y[q][a], yh[q], t);
+                        if (BOUNDED) t += pex[a];
+                        pv[a] = t;
+#pragma unroll
+                        for (int b = (a < NX ? NX : a); b < NS; ++b) {
+                            FT v = (FT)((a == b) ? R[a - NX] : 0.0);
+#pragma unroll
+                            for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
+                            PS(a, b) = v;
+                        }
+                    }
+                }
+            }
+            MMPC_PHASE(2);
+            if (pass == 0) {
+                kkt = fmax(gmax, cmax);
+                if (trc) {
+                    trc[0] = gmax;
+                    trc[1] = cmax;
+                    trc[2] = J0;
+                    trc[3] = c1;
+                    trc[7] = lmax;
+                }
+                if (nonfinite || !isfinite(kkt)) {
+                    status = ST_NONFINITE;
+                    done = true;
+                    break;
+                }
+                if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
+                    status = ST_CONVERGED;
+                    done = true;
+                    break;
+                }
+                if (it == p.max_iter) {
+                    status = ST_MAX_ITER;
+                    done = true;
+                    break;
+                }
+                if (BOUNDED) pg_prev = gmax;
+            }
+            if (!fact_ok) {
+                status = ST_FACT_FAILED;
+                done = true;
+                break;
+            }
+
+            // ---- (3) forward: step (dx, du) and the directional derivative of J ----
+            dJ = 0.0;
+            {
+                double dx[NX], dup[NU], um[NU];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    dx[r] = 0.0;
+                    ST(0, SF::DX, r) = 0.0;
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    dup[c] = 0.0;
+                    um[c] = up[c];
+                }
+                // software pipeline as in (1); the feedback gains K_k are consumed (and loaded) before the model
+                // evaluation, whose compute then covers the remaining loads of the stage
+                double xpf[NX], upf[NU];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) xpf[r] = ST(0, SF::X, r);
+#pragma unroll
+                for (int c = 0; c < NU; ++c) upf[c] = ST(0, SF::U, c);
+                #pragma unroll 1
+                for (int k = 0; k < N; ++k) {
+                    double* const sk = stage_ptr(wsb, k, SS, lane);
+                    double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        x[r] = xpf[r];
+                        xpf[r] = SK(1, SF::X, r);
+                        rk[r] = SK(0, SF::R, r);
+                        ck[r] = SK(0, SF::C, r);
+                    }
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {
+                        u[c] = upf[c];
+                        upf[c] = SK(1, SF::U, c);  // stage N's U slot exists (unused) when k = N-1
+                    }
+                    double du[NU];
+                    const double* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
+                    const FT* const kk = reinterpret_cast<const FT*>(kb + NU * 64) + lane;
 #pragma unroll
                     for (int a = 0; a < NU; ++a) {
-                        kb[a * 64 + lane] = -kh[a];
+                        const int base = a * NS;
+                        double t = kb[a * 64 + lane];
 #pragma unroll
-                        for (int j = 0; j < NS; ++j) kk[(a * NS + j) * 64] = -Kt[a][j];
+                        for (int q = 0; q < NX; ++q) t = fma((double)kk[(base + q) * 64], dx[q], t);
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) t = fma((double)kk[(base + NX + c) * 64], dup[c], t);
+                        du[a] = t;
+                        SK(0, SF::DU, a) = t;
                     }
-                }
-                if (k == 0) break;  // s_0 = 0: P~_0 is never used
-                // P~_k = blkdiag(A^T W + Q, R) - Y^T Y (old P is dead: overwrite it in place), p~_k = pn - Y^T yh
-                asm volatile("" ::: "memory");  // W comes back from memory, not from forwarded registers
+                    if (BOUNDED && pass + 1 < kBoundPasses) {  // a free control whose step crosses a bound: hold it
 #pragma unroll
-                for (int b = 0; b < NX; ++b) {
-                    FT wcol[NX], col[NX];
-#pragma unroll
-                    for (int r = 0; r < NX; ++r) wcol[r] = sw[(r * NX + b) * 64];
-                    at_mul<NQ, FT>(hf, fq, fqd, wcol, col);
-#pragma unroll
-                    for (int a = 0; a <= b; ++a) {
-                        FT v = col[a] + (FT)((a == b) ? Q[a] : 0.0);
-#pragma unroll
-                        for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
-                        PS(a, b) = v;
+                        for (int a = 0; a < NU; ++a) {
+                            const double hv = SK(0, SF::HOLD, a), t = u[a] + du[a];
+                            if (hv != hv && (t < lbv[a] || t > ubv[a])) {
+                                SK(0, SF::HOLD, a) = t < lbv[a] ? lbv[a] : ubv[a];
+                                resolve = true;
+                            }
+                        }
                     }
-                }
+                    STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                    double ad[NX];
+                    a_mul<NQ>(h, hFq, hFqd, dx, ad);
 #pragma unroll
-                for (int a = 0; a < NS; ++a) {
-                    double t = pn[a];
+                    for (int s = 0; s < NQ; ++s)
 #pragma unroll
-                    for (int q = 0; q < NU; ++q) t = fma(-(double)Y[q][a], yh[q], t);
-                    pv[a] = t;
+                        for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
 #pragma unroll
-                    for (int b = (a < NX ? NX : a); b < NS; ++b) {
-                        FT v = (FT)((a == b) ? R[a - NX] : 0.0);
+                    for (int r = 0; r < NX; ++r) {
+                        const double F = fma(h, xd[r], x[r]);
+                        const double qe = 2.0 * Q[r] * (F - rk[r]);
+                        dJ = fma(qe, ad[r], dJ);
+                        dx[r] = ad[r] + ck[r];
+                        SK(1, SF::DX, r) = dx[r];
+                    }
 #pragma unroll
-                        for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
-                        PS(a, b) = v;
+                    for (int c = 0; c < NU; ++c) {
+                        const double dif = u[c] - um[c];
+                        dJ = fma(2.0 * R[c] * dif, du[c] - dup[c], fma(2.0 * Rm[c] * u[c], du[c], dJ));
+                        um[c] = u[c];
+                        dup[c] = du[c];
                     }
                 }
             }
-        }
-        MMPC_PHASE(2);
-        kkt = fmax(gmax, cmax);
-        // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
-        double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
-        if (trc) {
-            trc[0] = gmax;
-            trc[1] = cmax;
-            trc[2] = J0;
-            trc[3] = c1;
-            trc[7] = lmax;
-        }
-        if (nonfinite || !isfinite(kkt)) {
-            status = ST_NONFINITE;
-            break;
-        }
-        if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
-            status = ST_CONVERGED;
-            break;
-        }
-        if (it == p.max_iter) {
-            status = ST_MAX_ITER;
-            break;
-        }
-        if (!fact_ok) {
-            status = ST_FACT_FAILED;
-            break;
-        }
 
-        // ---- (3) forward: step (dx, du) and the directional derivative of J ----
-        double dJ = 0.0;
-        {
-            double dx[NX], dup[NU], um[NU];
-#pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                dx[r] = 0.0;
-                ST(0, SF::DX, r) = 0.0;
-            }
-#pragma unroll
-            for (int c = 0; c < NU; ++c) {
-                dup[c] = 0.0;
-                um[c] = up[c];
-            }
-            // software pipeline as in (1); the feedback gains K_k are consumed (and loaded) before the model
-            // evaluation, whose compute then covers the remaining loads of the stage
-            double xpf[NX], upf[NU];
-#pragma unroll
-            for (int r = 0; r < NX; ++r) xpf[r] = ST(0, SF::X, r);
-#pragma unroll
-            for (int c = 0; c < NU; ++c) upf[c] = ST(0, SF::U, c);
-            #pragma unroll 1
-            for (int k = 0; k < N; ++k) {
-                double* const sk = stage_ptr(wsb, k, SS, lane);
-                double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
-#pragma unroll
-                for (int r = 0; r < NX; ++r) {
-                    x[r] = xpf[r];
-                    xpf[r] = SK(1, SF::X, r);
-                    rk[r] = SK(0, SF::R, r);
-                    ck[r] = SK(0, SF::C, r);
-                }
-#pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    u[c] = upf[c];
-                    upf[c] = SK(1, SF::U, c);  // stage N's U slot exists (unused) when k = N-1
-                }
-                double du[NU];
-                const double* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
-                const FT* const kk = reinterpret_cast<const FT*>(kb + NU * 64) + lane;
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    const int base = a * NS;
-                    double t = kb[a * 64 + lane];
-#pragma unroll
-                    for (int q = 0; q < NX; ++q) t = fma((double)kk[(base + q) * 64], dx[q], t);
-#pragma unroll
-                    for (int c = 0; c < NU; ++c) t = fma((double)kk[(base + NX + c) * 64], dup[c], t);
-                    du[a] = t;
-                    SK(0, SF::DU, a) = t;
-                }
-                STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
-                double ad[NX];
-                a_mul<NQ>(h, hFq, hFqd, dx, ad);
-#pragma unroll
-                for (int s = 0; s < NQ; ++s)
-#pragma unroll
-                    for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
-#pragma unroll
-                for (int r = 0; r < NX; ++r) {
-                    const double F = fma(h, xd[r], x[r]);
-                    const double qe = 2.0 * Q[r] * (F - rk[r]);
-                    dJ = fma(qe, ad[r], dJ);
-                    dx[r] = ad[r] + ck[r];
-                    SK(1, SF::DX, r) = dx[r];
-                }
-#pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    const double dif = u[c] - um[c];
-                    dJ = fma(2.0 * R[c] * dif, du[c] - dup[c], fma(2.0 * Rm[c] * u[c], du[c], dJ));
-                    um[c] = u[c];
-                    dup[c] = du[c];
-                }
-            }
+            MMPC_PHASE(4);
+            if (!BOUNDED || !resolve || pass + 1 >= kBoundPasses) break;
         }
-
-        MMPC_PHASE(4);
+        if (done) break;
         // ---- (4) l1-merit Armijo line search (noise-aware, as sqp_wave.h) ----
         mu = fmax(mu, 4.0 * lmax + 1.0);
         const double phi0 = fma(mu, c1, J0);
@@ -670,6 +753,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
                     u[c] = fma(alpha, dupf[c], upf[c]);
+                    if (BOUNDED) u[c] = proj(u[c], lbv[c], ubv[c]);  // projected trial point
                     upf[c] = SK(1, SF::U, c);   // software pipeline as in (1)
                     dupf[c] = SK(1, SF::DU, c);
                 }
@@ -724,24 +808,15 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             }
             if (k < N) {
 #pragma unroll
-                for (int c = 0; c < NU; ++c) SK(0, SF::U, c) = fma(alpha, SK(0, SF::DU, c), SK(0, SF::U, c));
+                for (int c = 0; c < NU; ++c) {
+                    const double un = fma(alpha, SK(0, SF::DU, c), SK(0, SF::U, c));
+                    SK(0, SF::U, c) = BOUNDED ? proj(un, lbv[c], ubv[c]) : un;
+                }
             }
         }
     }
 
     MMPC_PHASE(6);
-    // ---- bounds check (box constraints are reported, not yet enforced), as sqp_wave.h ----
-    if (status == ST_CONVERGED && (p.u_lb || p.u_ub)) {
-        bool viol = false;
-        for (int k = 0; k < N; ++k)
-#pragma unroll
-            for (int r = 0; r < NU; ++r) {
-                const double u = ST(k, SF::U, r);
-                if (p.u_lb) viol |= (p.u_lb[r] > -1e19) && (u < p.u_lb[r] - 1e-9);
-                if (p.u_ub) viol |= (p.u_ub[r] < 1e19) && (u > p.u_ub[r] + 1e-9);
-            }
-        if (viol) status = ST_BOUNDS;
-    }
     // ---- write back V (reference layout) ----
     double* Vout = p.V + inst * (int64_t)NV;
     for (int k = 0; k < N; ++k) {

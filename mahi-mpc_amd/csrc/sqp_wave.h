@@ -59,8 +59,31 @@ enum {
     ST_LS_FAILED = 2,
     ST_NONFINITE = 3,
     ST_FACT_FAILED = 4,
-    ST_BOUNDS = 5
+    ST_BOUNDS = 5  // reserved: u bounds are enforced, never reported
 };
+
+// ---------------- box constraints on u (ModelControl.cpp:37-50,146-157), projected GN-SQP ----------------
+// Same rule as oracle/mmpc_oracle.c solve_one: controls within eps = min(kBoundEps, previous projected
+// gradient) of a bound with the gradient pointing outward are held at that bound in the QP (Bertsekas'
+// epsilon-active set), a free control whose step crosses a bound is held there and the QP solved again (at
+// most kBoundPasses solves per iteration), trial points are projected, and the stop test uses
+// ||U - P(U - 2g)||_inf.  Kernels take a BOUNDED template flag so that the unbounded code is unchanged.
+constexpr double kBoundEps = 1e-6;
+constexpr int kBoundPasses = 4;
+__device__ __forceinline__ double proj(double v, double lb, double ub) { return v < lb ? lb : (v > ub ? ub : v); }
+// bound values of |b| >= 1e19 are infinite (IPOPT's convention); NaN marks a free control in hold fields
+template <int NU, bool BOUNDED>
+__device__ __forceinline__ void load_bounds(const SolveParams& p, double* lbv, double* ubv) {
+#pragma unroll
+    for (int c = 0; c < NU; ++c) {
+        lbv[c] = -INFINITY;
+        ubv[c] = INFINITY;
+        if (BOUNDED) {
+            if (p.u_lb && p.u_lb[c] > -1e19) lbv[c] = p.u_lb[c];
+            if (p.u_ub && p.u_ub[c] < 1e19) ubv[c] = p.u_ub[c];
+        }
+    }
+}
 
 // ---------------- wave helpers ----------------
 // Pin a value at this point of the instruction stream.  Without it the optimiser sinks the
@@ -143,7 +166,7 @@ __device__ unsigned long long g_mmpc_phase_cycles[16];
 #endif
 
 // ---------------- the kernel ----------------
-template <class Model, int NMAX>
+template <class Model, int NMAX, bool BOUNDED = false>
 __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(SolveParams p) {
     constexpr int NX = Model::NX, NU = Model::NU, ND = NX + NU;
     constexpr int MMAX = NMAX * NU;
@@ -177,6 +200,15 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
     const int NV = NX * (N + 1) + NU * N;
     const double hstep = p.h;
 
+    double lbv[NU], ubv[NU];
+    load_bounds<NU, BOUNDED>(p, lbv, ubv);
+    // bounds of the control a Hessian-row lane owns (input lane % NU)
+    double lb_row = lbv[0], ub_row = ubv[0];
+#pragma unroll
+    for (int c = 1; c < NU; ++c) {
+        lb_row = (lane % NU == c) ? lbv[c] : lb_row;
+        ub_row = (lane % NU == c) ? ubv[c] : ub_row;
+    }
     // ---- load the instance (the only HBM reads of the solve) ----
     const double* w = p.weights + inst * p.w_stride;
     if (lane < NX + 2 * NU) sW[lane] = w[lane];
@@ -201,6 +233,10 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
     if (lane < NX) sX[lane] = p.x0[inst * NX + lane];  // x_0 pinned (ModelControl.cpp:144-145)
     if (lane < NU) sUp[lane] = p.u_prev[inst * NU + lane];
     __syncthreads();
+    if (BOUNDED) {  // the iterate starts projected onto the box
+        if (lane < M) sU[lane] = proj(sU[lane], lb_row, ub_row);
+        __syncthreads();
+    }
     double up[NU];
 #pragma unroll
     for (int c = 0; c < NU; ++c) up[c] = sUp[c];
@@ -224,7 +260,7 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
 
     int status = ST_MAX_ITER;
     int it = 0;
-    double kkt = 0.0, mu = 0.0;
+    double kkt = 0.0, mu = 0.0, pg_prev = INFINITY;
     MMPC_PHASE(0);
 
     for (it = 0; it <= p.max_iter; ++it) {
@@ -313,301 +349,353 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
         __syncthreads();
         MMPC_PHASE(2);
 
-        // ---- 3+4+5a. one backward sweep over the stages, j = NMAX-1 .. 0 ----
-        //   lanes 0..15  (row 0): P_{j+1}[pa][pb] -> P_j = Q + A_j^T P_{j+1} A_j, Z_{j-1} = B_{j-1}^T P_j
-        //                         (rows of P/T via quad_perm, columns via row_ror:4/8/12)
-        //   lanes 16..19 (quad 4): adjoint lam_j = Q e_{j-1} + A_j^T lam_{j+1}
-        //   all lanes           : lower half of the condensed Hessian row (stage si, input sr),
-        //                         t_j = t_{j+1} A_{j+1} + d_j Z_j[sr],  H_ij = t_j B_j   (d_j = [j == si])
-        // The serial P / lam chains are latency-bound; the Hessian row work fills their gaps.  Stages
-        // >= N are structurally zero (A = B = e = 0), so P_j = Q and lam_j = 0 there.  Z_j goes through
-        // LDS (lanes 0..7 write, every lane reads its row one step later; same-wave LDS order).
-        const int si = lane / NU, sr = lane - (lane / NU) * NU;  // Hessian row lane = (stage si, input sr)
-        const bool row_valid = lane < M;
-        double hrow[MMAX];
-        double lmax;
-        const double Rr = sW[NX + sr], Rmr = sW[NX + NU + sr];
-        const double dterm = Rr * ((si + 1 < N) ? 2.0 : 1.0) + Rmr;
-        double wdiag[NU], woff[NU];
+        // Steps 3-7 run once, or (bounded) again after holding controls whose step crosses a bound.
+        bool done = false;
+        double lmax = 0.0;
+        double tgt = NAN;  // bounded: the bound this lane's control (Hessian row) is held at, NaN = free
+        const double beps = BOUNDED ? fmin(kBoundEps, pg_prev) : 0.0;
+        double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
+        for (int pass = 0;; ++pass) {
+            // ---- 3+4+5a. one backward sweep over the stages, j = NMAX-1 .. 0 ----
+            //   lanes 0..15  (row 0): P_{j+1}[pa][pb] -> P_j = Q + A_j^T P_{j+1} A_j, Z_{j-1} = B_{j-1}^T P_j
+            //                         (rows of P/T via quad_perm, columns via row_ror:4/8/12)
+            //   lanes 16..19 (quad 4): adjoint lam_j = Q e_{j-1} + A_j^T lam_{j+1}
+            //   all lanes           : lower half of the condensed Hessian row (stage si, input sr),
+            //                         t_j = t_{j+1} A_{j+1} + d_j Z_j[sr],  H_ij = t_j B_j   (d_j = [j == si])
+            // The serial P / lam chains are latency-bound; the Hessian row work fills their gaps.  Stages
+            // >= N are structurally zero (A = B = e = 0), so P_j = Q and lam_j = 0 there.  Z_j goes through
+            // LDS (lanes 0..7 write, every lane reads its row one step later; same-wave LDS order).
+            const int si = lane / NU, sr = lane - (lane / NU) * NU;  // Hessian row lane = (stage si, input sr)
+            const bool row_valid = lane < M;
+            double hrow[MMAX];
+            const double Rr = sW[NX + sr], Rmr = sW[NX + NU + sr];
+            const double dterm = Rr * ((si + 1 < N) ? 2.0 : 1.0) + Rmr;
+            double wdiag[NU], woff[NU];
 #pragma unroll
-        for (int c = 0; c < NU; ++c) {
-            wdiag[c] = (c == sr) ? dterm : 0.0;
-            woff[c] = (c == sr) ? -Rr : 0.0;
-        }
-        {
-            const int pa = (lane >> 2) & 3, pb = lane & 3;
-            // row index of the value each lane receives from row_ror:4s (s = 1,2,3)
-            const int c1 = (row_rot4_src<1>(lane) >> 2) & 3;
-            const int c2 = (row_rot4_src<2>(lane) >> 2) & 3;
-            const int c3 = (row_rot4_src<3>(lane) >> 2) & 3;
-            const bool lam_lane = (lane >> 2) == 4;
-            const bool z_lane = lane < 16 && pa < NU;
-            const int zr = pa < NU ? pa : NU - 1;
-            const double pq = (pa == pb) ? sW[pa] : 0.0;
-            double P = pq;                                   // P_NMAX = Q
-            double lam = Qa * sE[(NMAX - 1) * NX + qa];      // lam_NMAX (e_j = 0 for j >= N)
-            if (lam_lane) sLam[NMAX * NX + qa] = lam;
-            lmax = lam_lane ? fabs(lam) : 0.0;
-            {   // Z_{NMAX-1} = B^T Q
-                const double* Bi = sB + (NMAX - 1) * NX * NU;
-                const double P1 = row_rot4<1>(P), P2 = row_rot4<2>(P), P3 = row_rot4<3>(P);
-                const double z = fma(Bi[c3 * NU + zr], P3, fma(Bi[c2 * NU + zr], P2,
-                                     fma(Bi[c1 * NU + zr], P1, Bi[pa * NU + zr] * P)));
-                if (z_lane) sZ[(NMAX - 1) * NU * NX + pa * NX + pb] = z;
+            for (int c = 0; c < NU; ++c) {
+                wdiag[c] = (c == sr) ? dterm : 0.0;
+                woff[c] = (c == sr) ? -Rr : 0.0;
             }
-            double t[NX] = {0.0, 0.0, 0.0, 0.0};
-            double dprev = 0.0;  // d_{j+1}
-#pragma unroll
-            for (int j = NMAX - 1; j >= 0; --j) {
-                int jj = j;
-                asm volatile("" : "+s"(jj));
-                const double dj = (si == jj) ? 1.0 : 0.0;
-                // (a) Hessian row, lower part
-                {
-                    const double2* zp = reinterpret_cast<const double2*>(sZ + j * NU * NX + sr * NX);
-                    const double2 z01 = zp[0], z23 = zp[1];
-                    const double zz[NX] = {z01.x, z01.y, z23.x, z23.y};
-                    if (j < NMAX - 1) {
-                        const double* A1 = sA + (j + 1) * NX * NX;
-                        double tn[NX];
-#pragma unroll
-                        for (int q = 0; q < NX; ++q)
-                            tn[q] = fma(dj, zz[q], fma(t[3], A1[3 * NX + q], fma(t[2], A1[2 * NX + q],
-                                                       fma(t[1], A1[1 * NX + q], t[0] * A1[0 * NX + q]))));
-#pragma unroll
-                        for (int q = 0; q < NX; ++q) t[q] = tn[q];
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < NX; ++q) t[q] = dj * zz[q];
-                    }
-                    const double* Bj = sB + j * NX * NU;
-#pragma unroll
-                    for (int c = 0; c < NU; ++c) {
-                        const double base = fma(dprev, woff[c], dj * wdiag[c]);
-                        hrow[j * NU + c] = fma(t[3], Bj[3 * NU + c],
-                                               fma(t[2], Bj[2 * NU + c], fma(t[1], Bj[1 * NU + c], fma(t[0], Bj[0 * NU + c], base))));
-                        MMPC_PIN(hrow[j * NU + c]);
-                    }
-#pragma unroll
-                    for (int q = 0; q < NX; ++q) MMPC_PIN(t[q]);
-                    dprev = dj;
-                }
-                // (b) P_j = Q + A_j^T (P_{j+1} A_j), lam_j
-                {
-                    const double* Ai = sA + j * NX * NX;
-                    double aT[4];
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) aT[c] = Ai[c * NX + pb];  // column pb (= qa) of A_j
-                    const double r0 = quad_bcast<0>(P), r1 = quad_bcast<1>(P), r2 = quad_bcast<2>(P), r3 = quad_bcast<3>(P);
-                    const double T = fma(r0, aT[0], r1 * aT[1]) + fma(r2, aT[2], r3 * aT[3]);
-                    const double T1 = row_rot4<1>(T), T2 = row_rot4<2>(T), T3 = row_rot4<3>(T);
-                    P = pq + (fma(Ai[pa * NX + pa], T, Ai[c1 * NX + pa] * T1) +
-                              fma(Ai[c2 * NX + pa], T2, Ai[c3 * NX + pa] * T3));
-                    if (j >= 1) {
-                        const double l0 = quad_bcast<0>(lam), l1 = quad_bcast<1>(lam), l2 = quad_bcast<2>(lam),
-                                     l3 = quad_bcast<3>(lam);
-                        lam = fma(Qa, sE[(j - 1) * NX + qa], fma(aT[0], l0, aT[1] * l1) + fma(aT[2], l2, aT[3] * l3));
-                        if (lam_lane) {
-                            sLam[j * NX + qa] = lam;
-                            lmax = fmax(lmax, fabs(lam));
-                        }
-                    }
-                }
-                // (c) Z_{j-1} = B_{j-1}^T P_j for the next step's Hessian rows
-                if (j >= 1) {
-                    const double* Bi = sB + (j - 1) * NX * NU;
+            {
+                const int pa = (lane >> 2) & 3, pb = lane & 3;
+                // row index of the value each lane receives from row_ror:4s (s = 1,2,3)
+                const int c1 = (row_rot4_src<1>(lane) >> 2) & 3;
+                const int c2 = (row_rot4_src<2>(lane) >> 2) & 3;
+                const int c3 = (row_rot4_src<3>(lane) >> 2) & 3;
+                const bool lam_lane = (lane >> 2) == 4;
+                const bool z_lane = lane < 16 && pa < NU;
+                const int zr = pa < NU ? pa : NU - 1;
+                const double pq = (pa == pb) ? sW[pa] : 0.0;
+                double P = pq;                                   // P_NMAX = Q
+                double lam = Qa * sE[(NMAX - 1) * NX + qa];      // lam_NMAX (e_j = 0 for j >= N)
+                if (lam_lane) sLam[NMAX * NX + qa] = lam;
+                lmax = lam_lane ? fabs(lam) : 0.0;
+                {   // Z_{NMAX-1} = B^T Q
+                    const double* Bi = sB + (NMAX - 1) * NX * NU;
                     const double P1 = row_rot4<1>(P), P2 = row_rot4<2>(P), P3 = row_rot4<3>(P);
                     const double z = fma(Bi[c3 * NU + zr], P3, fma(Bi[c2 * NU + zr], P2,
                                          fma(Bi[c1 * NU + zr], P1, Bi[pa * NU + zr] * P)));
-                    if (z_lane) sZ[(j - 1) * NU * NX + pa * NX + pb] = z;
+                    if (z_lane) sZ[(NMAX - 1) * NU * NX + pa * NX + pb] = z;
                 }
-            }
-        }
-        __syncthreads();
-        MMPC_PHASE(4);
-        double g = 0.0;
-        if (row_valid) {
-            const double* ln = sLam + (si + 1) * NX;
+                double t[NX] = {0.0, 0.0, 0.0, 0.0};
+                double dprev = 0.0;  // d_{j+1}
 #pragma unroll
-            for (int q = 0; q < NX; ++q) g = fma(sB[si * NX * NU + q * NU + sr], ln[q], g);
-            const double ui = sU[si * NU + sr];
-            const double um = (si == 0) ? sUp[sr] : sU[(si - 1) * NU + sr];
-            g = fma(Rr, ui - um, fma(Rmr, ui, g));
-            if (si + 1 < N) g -= Rr * (sU[(si + 1) * NU + sr] - ui);
-            nonfinite |= !isfinite(g);
-        }
-        const double gmax = wave_max(fabs(2.0 * g));
-        kkt = fmax(gmax, cmax);
-        double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
-        if (trc && lane == 0) {
-            trc[0] = gmax;
-            trc[1] = cmax;
-        }
-        if (__any(nonfinite) || !isfinite(kkt)) {
-            status = ST_NONFINITE;
-            break;
-        }
-        if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
-            status = ST_CONVERGED;
-            break;
-        }
-        if (it == p.max_iter) {
-            status = ST_MAX_ITER;
-            break;
-        }
-        MMPC_PHASE(3);
-
-        // ---- 5b. condensed Hessian, upper part (j > si): w_j = A_j v_{j-1},  H_ij = Z_j w_j,
-        //      v_j = w_j + d_j b (w_j == 0 for j <= si).  The lower and upper parts never overlap, so they
-        //      simply add (no selects).  The D^T R D + Rm band (ModelGenerator.cpp:216-221) rides on the
-        //      same indicators: diagonal at d_j, sub/super diagonals at d_{j+1} (lower) and d_{j-1} (upper).
-        {
-            double bcol[NX];
+                for (int j = NMAX - 1; j >= 0; --j) {
+                    int jj = j;
+                    asm volatile("" : "+s"(jj));
+                    const double dj = (si == jj) ? 1.0 : 0.0;
+                    // (a) Hessian row, lower part
+                    {
+                        const double2* zp = reinterpret_cast<const double2*>(sZ + j * NU * NX + sr * NX);
+                        const double2 z01 = zp[0], z23 = zp[1];
+                        const double zz[NX] = {z01.x, z01.y, z23.x, z23.y};
+                        if (j < NMAX - 1) {
+                            const double* A1 = sA + (j + 1) * NX * NX;
+                            double tn[NX];
 #pragma unroll
-            for (int q = 0; q < NX; ++q) bcol[q] = row_valid ? sB[si * NX * NU + q * NU + sr] : 0.0;
-            double v[NX] = {0.0, 0.0, 0.0, 0.0};
-            double dprev = 0.0;  // d_{j-1}
+                            for (int q = 0; q < NX; ++q)
+                                tn[q] = fma(dj, zz[q], fma(t[3], A1[3 * NX + q], fma(t[2], A1[2 * NX + q],
+                                                           fma(t[1], A1[1 * NX + q], t[0] * A1[0 * NX + q]))));
 #pragma unroll
-            for (int j = 0; j < NMAX; ++j) {
-                int jj = j;
-                asm volatile("" : "+s"(jj));
-                const double dj = (si == jj) ? 1.0 : 0.0;
-                const double* Aj = sA + j * NX * NX;
-                double w[NX];
+                            for (int q = 0; q < NX; ++q) t[q] = tn[q];
+                        } else {
 #pragma unroll
-                for (int q = 0; q < NX; ++q)
-                    w[q] = fma(Aj[q * NX + 3], v[3], fma(Aj[q * NX + 2], v[2], fma(Aj[q * NX + 1], v[1], Aj[q * NX + 0] * v[0])));
-                const double* Zj = sZ + j * NU * NX;
+                            for (int q = 0; q < NX; ++q) t[q] = dj * zz[q];
+                        }
+                        const double* Bj = sB + j * NX * NU;
 #pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    hrow[j * NU + c] = fma(Zj[c * NX + 3], w[3],
-                                           fma(Zj[c * NX + 2], w[2], fma(Zj[c * NX + 1], w[1],
-                                               fma(Zj[c * NX + 0], w[0], fma(dprev, woff[c], hrow[j * NU + c])))));
-                    MMPC_PIN(hrow[j * NU + c]);
-                }
+                        for (int c = 0; c < NU; ++c) {
+                            const double base = fma(dprev, woff[c], dj * wdiag[c]);
+                            hrow[j * NU + c] = fma(t[3], Bj[3 * NU + c],
+                                                   fma(t[2], Bj[2 * NU + c], fma(t[1], Bj[1 * NU + c], fma(t[0], Bj[0 * NU + c], base))));
+                            MMPC_PIN(hrow[j * NU + c]);
+                        }
 #pragma unroll
-                for (int q = 0; q < NX; ++q) {
-                    v[q] = fma(dj, bcol[q], w[q]);
-                    MMPC_PIN(v[q]);
-                }
-                dprev = dj;
-            }
-        }
-        MMPC_PHASE(5);
-        // ---- 6. Gauss-Jordan on [H | -g] ----
-        // The trailing block stays symmetric under elimination, so the pivot ROW entries a_kj (j > k)
-        // equal the pivot COLUMN entries a_jk that lane j holds in register k: one ds_write_b64 per step
-        // publishes the pivot row, and every update is an FMA with a broadcast LDS operand.  The row is
-        // written at an offset that makes every pair (k+1+2q, k+2+2q) 16-byte aligned (ds_read_b128), and
-        // the reads run two 8-value chunks ahead of the FMAs (LDS latency hidden inside the wave).
-        double rhs = row_valid ? -g : 0.0;
-        bool fact_bad = false;
-#pragma unroll
-        for (int k = 0; k < MMAX; ++k) {
-            if (k < M) {
-                constexpr int CH = 8;
-                double* piv = sPiv + (((k & 1) ^ 1));  // (k+1+off) even -> aligned pairs
-                const double col = hrow[k];
-                piv[lane] = col;
-                __builtin_amdgcn_wave_barrier();
-                int ko = k;  // opaque copy: keeps the lane == k compare inside this step (no SGPR-mask hoisting)
-                asm volatile("" : "+s"(ko));
-                const double akk = reinterpret_cast<const double2*>(sPiv)[(((k & 1) ^ 1) + k - 1) >> 1].y;
-                const int NCH = (MMAX - 1 - k + CH - 1) / CH;
-                const double2* piv2 = reinterpret_cast<const double2*>(sPiv);  // 16-B aligned pairs
-                const int off = (k & 1) ^ 1;
-                double preA[CH], preB[CH];
-#pragma unroll
-                for (int q = 0; q < CH; q += 2) {
-                    const int j0 = k + 1 + q, j1 = k + 1 + CH + q;
-                    if (j0 < MMAX) {
-                        const double2 v = piv2[(off + j0) >> 1];
-                        preA[q] = v.x;
-                        preA[q + 1] = v.y;
+                        for (int q = 0; q < NX; ++q) MMPC_PIN(t[q]);
+                        dprev = dj;
                     }
-                    if (j1 < MMAX) {
-                        const double2 v = piv2[(off + j1) >> 1];
-                        preB[q] = v.x;
-                        preB[q + 1] = v.y;
-                    }
-                }
-                fact_bad |= !(akk > 0.0) || !isfinite(akk);
-                const double inv = rcp_nr(akk);
-                const double mlt = (lane == ko) ? 0.0 : col * inv;
-                if (lane == 0) sDiag[k] = akk;
-                rhs = fma(-mlt, readlane_d(rhs, k), rhs);
+                    // (b) P_j = Q + A_j^T (P_{j+1} A_j), lam_j
+                    {
+                        const double* Ai = sA + j * NX * NX;
+                        double aT[4];
 #pragma unroll
-                for (int c = 0; c < NCH; ++c) {
-                    double cur[CH];
-#pragma unroll
-                    for (int q = 0; q < CH; ++q) cur[q] = (c & 1) ? preB[q] : preA[q];
-#pragma unroll
-                    for (int q = 0; q < CH; q += 2) {
-                        const int jn = k + 1 + (c + 2) * CH + q;  // refill the buffer just consumed
-                        if (c + 2 < NCH && jn < MMAX) {
-                            const double2 v = piv2[(off + jn) >> 1];
-                            if (c & 1) {
-                                preB[q] = v.x;
-                                preB[q + 1] = v.y;
-                            } else {
-                                preA[q] = v.x;
-                                preA[q + 1] = v.y;
+                        for (int c = 0; c < 4; ++c) aT[c] = Ai[c * NX + pb];  // column pb (= qa) of A_j
+                        const double r0 = quad_bcast<0>(P), r1 = quad_bcast<1>(P), r2 = quad_bcast<2>(P), r3 = quad_bcast<3>(P);
+                        const double T = fma(r0, aT[0], r1 * aT[1]) + fma(r2, aT[2], r3 * aT[3]);
+                        const double T1 = row_rot4<1>(T), T2 = row_rot4<2>(T), T3 = row_rot4<3>(T);
+                        P = pq + (fma(Ai[pa * NX + pa], T, Ai[c1 * NX + pa] * T1) +
+                                  fma(Ai[c2 * NX + pa], T2, Ai[c3 * NX + pa] * T3));
+                        if (j >= 1) {
+                            const double l0 = quad_bcast<0>(lam), l1 = quad_bcast<1>(lam), l2 = quad_bcast<2>(lam),
+                                         l3 = quad_bcast<3>(lam);
+                            lam = fma(Qa, sE[(j - 1) * NX + qa], fma(aT[0], l0, aT[1] * l1) + fma(aT[2], l2, aT[3] * l3));
+                            if (lam_lane) {
+                                sLam[j * NX + qa] = lam;
+                                lmax = fmax(lmax, fabs(lam));
                             }
                         }
                     }
-#pragma unroll
-                    for (int q = 0; q < CH; ++q) {
-                        const int j = k + 1 + c * CH + q;
-                        if (j < MMAX) hrow[j] = fma(-mlt, cur[q], hrow[j]);
+                    // (c) Z_{j-1} = B_{j-1}^T P_j for the next step's Hessian rows
+                    if (j >= 1) {
+                        const double* Bi = sB + (j - 1) * NX * NU;
+                        const double P1 = row_rot4<1>(P), P2 = row_rot4<2>(P), P3 = row_rot4<3>(P);
+                        const double z = fma(Bi[c3 * NU + zr], P3, fma(Bi[c2 * NU + zr], P2,
+                                             fma(Bi[c1 * NU + zr], P1, Bi[pa * NU + zr] * P)));
+                        if (z_lane) sZ[(j - 1) * NU * NX + pa * NX + pb] = z;
                     }
                 }
-                __builtin_amdgcn_wave_barrier();
             }
-        }
-        if (fact_bad) {
-            status = ST_FACT_FAILED;
-            break;
-        }
-        __syncthreads();
-        const double du = row_valid ? rhs / sDiag[lane] : 0.0;
-        if (row_valid) sDU[lane] = du;
-        __syncthreads();
-        MMPC_PHASE(6);
+            __syncthreads();
+            MMPC_PHASE(4);
+            double g = 0.0;
+            if (row_valid) {
+                const double* ln = sLam + (si + 1) * NX;
+#pragma unroll
+                for (int q = 0; q < NX; ++q) g = fma(sB[si * NX * NU + q * NU + sr], ln[q], g);
+                const double ui = sU[si * NU + sr];
+                const double um = (si == 0) ? sUp[sr] : sU[(si - 1) * NU + sr];
+                g = fma(Rr, ui - um, fma(Rmr, ui, g));
+                if (si + 1 < N) g -= Rr * (sU[(si + 1) * NU + sr] - ui);
+                nonfinite |= !isfinite(g);
+            }
+            double gmax;
+            if (!BOUNDED) {
+                gmax = wave_max(fabs(2.0 * g));
+            } else {  // projected gradient; hold rule (pass 0), later passes keep their holds
+                const double ur = row_valid ? sU[lane] : 0.0;
+                gmax = wave_max(row_valid ? fabs(ur - proj(ur - 2.0 * g, lb_row, ub_row)) : 0.0);
+                if (pass == 0)
+                    tgt = !row_valid                                ? NAN
+                          : (ur <= lb_row + beps && g > 0.0)   ? lb_row
+                          : (ur >= ub_row - beps && g < 0.0)   ? ub_row
+                                                               : NAN;
+            }
+            if (pass == 0) {
+                kkt = fmax(gmax, cmax);
+                if (trc && lane == 0) {
+                    trc[0] = gmax;
+                    trc[1] = cmax;
+                }
+                if (__any(nonfinite) || !isfinite(kkt)) {
+                    status = ST_NONFINITE;
+                    done = true;
+                    break;
+                }
+                if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
+                    status = ST_CONVERGED;
+                    done = true;
+                    break;
+                }
+                if (it == p.max_iter) {
+                    status = ST_MAX_ITER;
+                    done = true;
+                    break;
+                }
+                if (BOUNDED) pg_prev = gmax;
+            }
+            MMPC_PHASE(3);
 
-        // ---- 7. dx forward ----
-        {
-            double dx = 0.0;
-            if (lane < NX) sDX[qa] = 0.0;
-            auto ld = [&](int k, double2& a01, double2& a23, double2& b01, double& cc, double2& du01) {
-                a01 = reinterpret_cast<const double2*>(sA + k * NX * NX + qa * NX)[0];
-                a23 = reinterpret_cast<const double2*>(sA + k * NX * NX + qa * NX)[1];
-                b01 = reinterpret_cast<const double2*>(sB + k * NX * NU + qa * NU)[0];
-                cc = sC[k * NX + qa];
-                du01 = reinterpret_cast<const double2*>(sDU + k * NU)[0];
-            };
-            static_assert(NU == 2, "dx recursion packs the two controls of a stage");
-            double2 a01, a23, b01, du01;
-            double cc;
-            ld(0, a01, a23, b01, cc, du01);
-            for (int k = 0; k < N; ++k) {
-                double2 na01, na23, nb01, ndu01;
-                double ncc;
-                ld((k + 1 < N) ? k + 1 : k, na01, na23, nb01, ncc, ndu01);
-                const double x0v = quad_bcast<0>(dx), x1v = quad_bcast<1>(dx), x2v = quad_bcast<2>(dx),
-                             x3v = quad_bcast<3>(dx);
-                const double bu = fma(b01.x, du01.x, fma(b01.y, du01.y, cc));
-                const double dn = (fma(a01.x, x0v, a01.y * x1v) + fma(a23.x, x2v, a23.y * x3v)) + bu;
-                if (lane < NX) sDX[(k + 1) * NX + qa] = dn;
-                dx = dn;
-                a01 = na01;
-                a23 = na23;
-                b01 = nb01;
-                cc = ncc;
-                du01 = ndu01;
+            // ---- 5b. condensed Hessian, upper part (j > si): w_j = A_j v_{j-1},  H_ij = Z_j w_j,
+            //      v_j = w_j + d_j b (w_j == 0 for j <= si).  The lower and upper parts never overlap, so they
+            //      simply add (no selects).  The D^T R D + Rm band (ModelGenerator.cpp:216-221) rides on the
+            //      same indicators: diagonal at d_j, sub/super diagonals at d_{j+1} (lower) and d_{j-1} (upper).
+            {
+                double bcol[NX];
+#pragma unroll
+                for (int q = 0; q < NX; ++q) bcol[q] = row_valid ? sB[si * NX * NU + q * NU + sr] : 0.0;
+                double v[NX] = {0.0, 0.0, 0.0, 0.0};
+                double dprev = 0.0;  // d_{j-1}
+#pragma unroll
+                for (int j = 0; j < NMAX; ++j) {
+                    int jj = j;
+                    asm volatile("" : "+s"(jj));
+                    const double dj = (si == jj) ? 1.0 : 0.0;
+                    const double* Aj = sA + j * NX * NX;
+                    double w[NX];
+#pragma unroll
+                    for (int q = 0; q < NX; ++q)
+                        w[q] = fma(Aj[q * NX + 3], v[3], fma(Aj[q * NX + 2], v[2], fma(Aj[q * NX + 1], v[1], Aj[q * NX + 0] * v[0])));
+                    const double* Zj = sZ + j * NU * NX;
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {
+                        hrow[j * NU + c] = fma(Zj[c * NX + 3], w[3],
+                                               fma(Zj[c * NX + 2], w[2], fma(Zj[c * NX + 1], w[1],
+                                                   fma(Zj[c * NX + 0], w[0], fma(dprev, woff[c], hrow[j * NU + c])))));
+                        MMPC_PIN(hrow[j * NU + c]);
+                    }
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) {
+                        v[q] = fma(dj, bcol[q], w[q]);
+                        MMPC_PIN(v[q]);
+                    }
+                    dprev = dj;
+                }
             }
-        }
-        __syncthreads();
-        MMPC_PHASE(7);
+            MMPC_PHASE(5);
+            // ---- 6. Gauss-Jordan on [H | -g] ----
+            // The trailing block stays symmetric under elimination, so the pivot ROW entries a_kj (j > k)
+            // equal the pivot COLUMN entries a_jk that lane j holds in register k: one ds_write_b64 per step
+            // publishes the pivot row, and every update is an FMA with a broadcast LDS operand.  The row is
+            // written at an offset that makes every pair (k+1+2q, k+2+2q) 16-byte aligned (ds_read_b128), and
+            // the reads run two 8-value chunks ahead of the FMAs (LDS latency hidden inside the wave).
+            double rhs = row_valid ? -g : 0.0;
+            if (BOUNDED) {  // held rows: du_a = target - u_a fixed, the free rows' QP takes its coupling to the rhs
+                const bool held = tgt == tgt;
+                const double dl = held ? tgt - sU[lane] : 0.0;
+                const uint64_t hm = __ballot(held);
+                if (hm) {
+                    double t = 0.0;
+#pragma unroll
+                    for (int j = 0; j < MMAX; ++j) t = fma(hrow[j], readlane_d(dl, j), t);
+                    rhs = held ? dl : rhs - t;
+#pragma unroll
+                    for (int j = 0; j < MMAX; ++j)
+                        if (held || ((hm >> j) & 1)) hrow[j] = (j == lane) ? 1.0 : 0.0;
+                }
+            }
+            bool fact_bad = false;
+#pragma unroll
+            for (int k = 0; k < MMAX; ++k) {
+                if (k < M) {
+                    constexpr int CH = 8;
+                    double* piv = sPiv + (((k & 1) ^ 1));  // (k+1+off) even -> aligned pairs
+                    const double col = hrow[k];
+                    piv[lane] = col;
+                    __builtin_amdgcn_wave_barrier();
+                    int ko = k;  // opaque copy: keeps the lane == k compare inside this step (no SGPR-mask hoisting)
+                    asm volatile("" : "+s"(ko));
+                    const double akk = reinterpret_cast<const double2*>(sPiv)[(((k & 1) ^ 1) + k - 1) >> 1].y;
+                    const int NCH = (MMAX - 1 - k + CH - 1) / CH;
+                    const double2* piv2 = reinterpret_cast<const double2*>(sPiv);  // 16-B aligned pairs
+                    const int off = (k & 1) ^ 1;
+                    double preA[CH], preB[CH];
+#pragma unroll
+                    for (int q = 0; q < CH; q += 2) {
+                        const int j0 = k + 1 + q, j1 = k + 1 + CH + q;
+                        if (j0 < MMAX) {
+                            const double2 v = piv2[(off + j0) >> 1];
+                            preA[q] = v.x;
+                            preA[q + 1] = v.y;
+                        }
+                        if (j1 < MMAX) {
+                            const double2 v = piv2[(off + j1) >> 1];
+                            preB[q] = v.x;
+                            preB[q + 1] = v.y;
+                        }
+                    }
+                    fact_bad |= !(akk > 0.0) || !isfinite(akk);
+                    const double inv = rcp_nr(akk);
+                    const double mlt = (lane == ko) ? 0.0 : col * inv;
+                    if (lane == 0) sDiag[k] = akk;
+                    rhs = fma(-mlt, readlane_d(rhs, k), rhs);
+#pragma unroll
+                    for (int c = 0; c < NCH; ++c) {
+                        double cur[CH];
+#pragma unroll
+                        for (int q = 0; q < CH; ++q) cur[q] = (c & 1) ? preB[q] : preA[q];
+#pragma unroll
+                        for (int q = 0; q < CH; q += 2) {
+                            const int jn = k + 1 + (c + 2) * CH + q;  // refill the buffer just consumed
+                            if (c + 2 < NCH && jn < MMAX) {
+                                const double2 v = piv2[(off + jn) >> 1];
+                                if (c & 1) {
+                                    preB[q] = v.x;
+                                    preB[q + 1] = v.y;
+                                } else {
+                                    preA[q] = v.x;
+                                    preA[q + 1] = v.y;
+                                }
+                            }
+                        }
+#pragma unroll
+                        for (int q = 0; q < CH; ++q) {
+                            const int j = k + 1 + c * CH + q;
+                            if (j < MMAX) hrow[j] = fma(-mlt, cur[q], hrow[j]);
+                        }
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            if (fact_bad) {
+                status = ST_FACT_FAILED;
+                done = true;
+                break;
+            }
+            __syncthreads();
+            const double du = row_valid ? rhs / sDiag[lane] : 0.0;
+            if (row_valid) sDU[lane] = du;
+            __syncthreads();
+            MMPC_PHASE(6);
+
+            // ---- 7. dx forward ----
+            {
+                double dx = 0.0;
+                if (lane < NX) sDX[qa] = 0.0;
+                auto ld = [&](int k, double2& a01, double2& a23, double2& b01, double& cc, double2& du01) {
+                    a01 = reinterpret_cast<const double2*>(sA + k * NX * NX + qa * NX)[0];
+                    a23 = reinterpret_cast<const double2*>(sA + k * NX * NX + qa * NX)[1];
+                    b01 = reinterpret_cast<const double2*>(sB + k * NX * NU + qa * NU)[0];
+                    cc = sC[k * NX + qa];
+                    du01 = reinterpret_cast<const double2*>(sDU + k * NU)[0];
+                };
+                static_assert(NU == 2, "dx recursion packs the two controls of a stage");
+                double2 a01, a23, b01, du01;
+                double cc;
+                ld(0, a01, a23, b01, cc, du01);
+                for (int k = 0; k < N; ++k) {
+                    double2 na01, na23, nb01, ndu01;
+                    double ncc;
+                    ld((k + 1 < N) ? k + 1 : k, na01, na23, nb01, ncc, ndu01);
+                    const double x0v = quad_bcast<0>(dx), x1v = quad_bcast<1>(dx), x2v = quad_bcast<2>(dx),
+                                 x3v = quad_bcast<3>(dx);
+                    const double bu = fma(b01.x, du01.x, fma(b01.y, du01.y, cc));
+                    const double dn = (fma(a01.x, x0v, a01.y * x1v) + fma(a23.x, x2v, a23.y * x3v)) + bu;
+                    if (lane < NX) sDX[(k + 1) * NX + qa] = dn;
+                    dx = dn;
+                    a01 = na01;
+                    a23 = na23;
+                    b01 = nb01;
+                    cc = ncc;
+                    du01 = ndu01;
+                }
+            }
+            __syncthreads();
+            MMPC_PHASE(7);
+            bool resolve = false;
+            if (BOUNDED && pass + 1 < kBoundPasses) {  // a free control whose step crosses a bound: hold it, solve again
+                bool add = false;
+                if (row_valid && tgt != tgt) {
+                    const double t = sU[lane] + sDU[lane];
+                    if (t < lb_row || t > ub_row) {
+                        tgt = t < lb_row ? lb_row : ub_row;
+                        add = true;
+                    }
+                }
+                resolve = __any(add);
+            }
+            if (!BOUNDED || !resolve || pass + 1 >= kBoundPasses) break;
+        }  // pass
+        if (done) break;
 
         // ---- 8. l1-merit Armijo line search ----
         mu = fmax(mu, 4.0 * wave_max(lmax) + 1.0);
@@ -653,7 +741,10 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
 #pragma unroll
                 for (int i = 0; i < NX; ++i) x[i] = fma(alpha, sDX[k * NX + i], sX[k * NX + i]);
 #pragma unroll
-                for (int i = 0; i < NU; ++i) u[i] = fma(alpha, sDU[k * NU + i], sU[k * NU + i]);
+                for (int i = 0; i < NU; ++i) {
+                    u[i] = fma(alpha, sDU[k * NU + i], sU[k * NU + i]);
+                    if (BOUNDED) u[i] = proj(u[i], lbv[i], ubv[i]);  // projected trial point
+                }
                 if (!p.is_linear) {
                     model_eval<Model>(x, u, xd);
                 } else {
@@ -676,7 +767,8 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
                 }
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
-                    const double um = (k == 0) ? up[c] : fma(alpha, sDU[(k - 1) * NU + c], sU[(k - 1) * NU + c]);
+                    double um = (k == 0) ? up[c] : fma(alpha, sDU[(k - 1) * NU + c], sU[(k - 1) * NU + c]);
+                    if (BOUNDED && k > 0) um = proj(um, lbv[c], ubv[c]);
                     const double dif = u[c] - um;
                     Jt = fma(dif * sW[NX + c], dif, fma(u[c] * sW[NX + NU + c], u[c], Jt));
                 }
@@ -703,7 +795,7 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
             trc[7] = accepted ? 1.0 : 0.0;
         }
         if (trc) {
-            const double dumax = wave_max(fabs(du));
+            const double dumax = wave_max(lane < M ? fabs(sDU[lane]) : 0.0);
             if (lane == 0) trc[6] = dumax;
         }
         if (!accepted) {
@@ -711,29 +803,14 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
             break;
         }
         for (int i = NX + lane; i < (N + 1) * NX; i += 64) sX[i] = fma(alpha, sDX[i], sX[i]);
-        if (lane < M) sU[lane] = fma(alpha, sDU[lane], sU[lane]);
+        if (lane < M) {
+            const double un = fma(alpha, sDU[lane], sU[lane]);
+            sU[lane] = BOUNDED ? proj(un, lb_row, ub_row) : un;
+        }
         __syncthreads();
         MMPC_PHASE(8);
     }
     MMPC_PHASE(3);
-
-    // ---- bounds check (box constraints are reported, not yet enforced) ----
-    if (status == ST_CONVERGED && (p.u_lb || p.u_ub)) {
-        bool viol = false;
-        if (lane < M) {
-            const int r = lane % NU;
-            const double u = sU[lane];
-            if (p.u_lb) {
-                const double lb = p.u_lb[r];
-                viol |= (lb > -1e19) && (u < lb - 1e-9);
-            }
-            if (p.u_ub) {
-                const double ub = p.u_ub[r];
-                viol |= (ub < 1e19) && (u > ub + 1e-9);
-            }
-        }
-        if (__any(viol)) status = ST_BOUNDS;
-    }
 
     // ---- write back V (reference layout) ----
     __syncthreads();

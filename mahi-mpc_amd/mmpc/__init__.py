@@ -80,6 +80,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise MmpcError(-2, f"{LIB_PATH} not built (run make -C mahi-mpc_amd)")
+        # PyTorch-ROCm ships its own HIP runtime: if libmmpc's initialises first, torch later sees no GPU
+        # (observed on the MI355X box), so torch -- when present -- initialises before the library is loaded
+        try:
+            import torch
+            torch.cuda.is_available()
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         L.mmpc_abi_version.restype = C.c_int
         L.mmpc_default_opts.argtypes = [C.POINTER(Opts)]

@@ -366,6 +366,9 @@ static int chol_solve(int M, double* H, double* b /* in: rhs, out: solution */) 
     return 0;
 }
 
+/* projection onto [lb, ub] that keeps a NaN a NaN (fmin/fmax would replace it by a bound) */
+static double proj(double v, double lb, double ub) { return v < lb ? lb : (v > ub ? ub : v); }
+
 static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, const double* traj,
                      const double* w, const double* u_lb, const double* u_ub, int max_iter,
                      double tol_grad, double tol_defect, double* V, int32_t* iters_out,
@@ -391,7 +394,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         has_b |= (lbv[q] > -INFINITY) || (ubv[q] < INFINITY);
     }
     if (has_b)
-        for (int a = 0; a < M; ++a) s->U[a] = fmin(fmax(s->U[a], lbv[a % NU]), ubv[a % NU]);
+        for (int a = 0; a < M; ++a) s->U[a] = proj(s->U[a], lbv[a % NU], ubv[a % NU]);
     double pg_prev = INFINITY;
 
     int status = ORACLE_MAX_ITER, it = 0;
@@ -469,7 +472,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
             const double eps = fmin(ORACLE_BOUND_EPS, pg_prev);
             for (int a = 0; a < M; ++a) {
                 const double u = s->U[a], lb = lbv[a % NU], ub = ubv[a % NU];
-                double t = fabs(u - fmin(fmax(u - 2.0 * s->g[a], lb), ub));
+                double t = fabs(u - proj(u - 2.0 * s->g[a], lb, ub));
                 if (t > gmax || t != t) gmax = t;
                 s->tgt[a] = (u <= lb + eps && s->g[a] > 0.0) ? lb : (u >= ub - eps && s->g[a] < 0.0) ? ub : NAN;
             }
@@ -569,7 +572,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
             for (int i = 0; i < (N + 1) * NX; ++i) s->Xt[i] = s->X[i] + alpha * s->dx[i];
             for (int i = 0; i < M; ++i) s->Ut[i] = s->U[i] + alpha * s->du[i];
             if (has_b)  /* projected trial point */
-                for (int i = 0; i < M; ++i) s->Ut[i] = fmin(fmax(s->Ut[i], lbv[i % NU]), ubv[i % NU]);
+                for (int i = 0; i < M; ++i) s->Ut[i] = proj(s->Ut[i], lbv[i % NU], ubv[i % NU]);
             double Jt, ct;
             merit_eval(N, h, s->Xt, s->Ut, u_prev, traj, w, s->Ft, &Jt, &ct);
             double phit = Jt + mu * ct;

@@ -214,7 +214,7 @@ def test_riccati_weights_bounds_nonfinite_warmstart(exo_solver, oracle):
     r2 = s.solve_batch_host(x0, up, tr, w, V=r["V"])            # warm start = fixed point
     assert (r2["iters"] == 0).all() and (r2["status"] == 0).all()
     np.testing.assert_array_equal(r2["V"], r["V"])
-    lb, ub = [-1e-3] * 4, [1e-3] * 4                             # bounds reported (status 5)
+    lb, ub = [-1e-3] * 4, [1e-3] * 4                             # bounds enforced
     r3 = s.solve_batch_host(x0[:8], up[:8], tr[:8], W_EXO, u_lb=lb, u_ub=ub)
     o3 = oracle.solve_batch(N, H, x0[:8], up[:8], tr[:8], W_EXO, u_lb=lb, u_ub=ub, model=oracle.EXO)
     np.testing.assert_array_equal(r3["status"], o3["status"])
