@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--kkt", choices=["auto", "condensed", "riccati", "group"], default="auto",
                     help="KKT solver (mmpc_opts.kkt_solver); auto = the library's choice")
     ap.add_argument("--horizon", type=int, default=None)
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: skip gathering the results to rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
@@ -113,8 +114,7 @@ def main():
     ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt]
     solver = mmpc.Solver(path, device=local, kkt_solver=ksolver)
     solver.reserve_workspace(B)
-    if ksolver == 0:
-        ksolver = 1 if (cfg["model"] == "two_link_arm" and N * nu <= 64) else 2
+    ksolver = solver.kkt_solver_for(B)   # the AUTO choice, resolved by the library
     riccati = ksolver in (2, 3)
     NV = solver.NV
     f64 = dict(dtype=torch.float64, device=dev)
@@ -129,6 +129,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     first, _ = mdist.shard(B, rank)
     solver.synth(SEED, first, B, x0, up, tr, stream=stream.cuda_stream)
+    mdist.broadcast_shared(w)   # shared weights from rank 0 (identical here by construction)
+    # N > 1: every step's per-instance results (u_0*, status, iterations) go to rank 0 -- one RCCL
+    # all_gather_into_tensor over xGMI per step, issued async so it overlaps the next step's solve
+    gather = mdist.ResultGather(B, nx, nu) if (world > 1 and not args.no_gather) else None
 
     def step():
         V.zero_()   # cold start (reference first call: v_init = 0, ModelControl.cpp:29-50)
@@ -147,6 +151,10 @@ def main():
         ev[k][0].record(stream)
         solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=stream.cuda_stream)
         ev[k][1].record(stream)
+        if gather:
+            gather.post(V, st, it)
+    if gather:
+        gather.wait()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -156,7 +164,13 @@ def main():
 
     iters = it.cpu().numpy()
     status = st.cpu().numpy()
-    conv = int(mdist.sum_over_ranks(int((status == 0).sum()), device=dev))
+    if gather:   # rank 0 holds every instance's result of the last step
+        last = gather.last()
+        gathered_ok = bool(torch.equal(last[rank * B:(rank + 1) * B, :nu], V[:, nx:nx + nu]))
+        conv = int((last[:, nu] == 0).sum().item())
+        gathered_ok = bool(mdist.sum_over_ranks(int(not gathered_ok), device=dev) == 0)
+    else:
+        conv = int(mdist.sum_over_ranks(int((status == 0).sum()), device=dev))
     total = B * world * args.steps
     value = total / elapsed
     # algorithmic flops of one launch = per-iteration figure x the SQP iterations the launch's instances
@@ -199,8 +213,11 @@ def main():
         "config": {"workload": cfg["workload"], "batch_per_gpu": B, "global_batch": B * world,
                    "horizon": N, "kkt_solver": {1: "condensed (wave per instance)", 2: "riccati (lane per instance)",
                                                 3: "riccati (16 lanes per instance)"}[ksolver],
-                   "parallelism": f"batch-shard x{world} (no data-path collective)"},
+                   "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) to rank 0 by "
+                                   "RCCL all_gather_into_tensor, overlapped with the next solve"
+                                   if gather else f"batch-shard x{world} (no collective on the solve path)")},
         "converged": conv,
+        **({"gathered_results_match": gathered_ok} if gather else {}),
         "mean_sqp_iters": float(iters.mean()),
         "kernel_ms": kern_ms,
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",

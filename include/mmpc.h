@@ -138,6 +138,10 @@ int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts);
  * stream-ordered solves allocate nothing; the workspace grows on demand otherwise).  *bytes (may be NULL) receives the workspace size. */
 int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes);
 
+/* The KKT solver (enum mmpc_kkt_solver) a solve of B instances runs under the handle's options:
+ * opts.kkt_solver, or what MMPC_KKT_AUTO picks for this model, horizon and B. */
+int mmpc_resolve_kkt_solver(const mmpc_handle* h, int64_t B, int32_t* solver);
+
 /* Batched SQP solve, DEVICE pointers, stream-ordered.  u_lb/u_ub: device [nu] or NULL
  * (unbounded; |bound| >= 1e19 is unbounded as in IPOPT).  Finite bounds are enforced (the lbx/ubx
  * of ModelControl.cpp:146-157): projected Gauss-Newton SQP, every returned u_k inside [u_lb, u_ub],

@@ -369,6 +369,20 @@ int set_dynamic_lds(K kernel, size_t bytes) {
     return MMPC_OK;
 }
 
+// the KKT solver a solve of B instances runs (opts.kkt_solver, or the AUTO choice)
+int resolve_kkt_solver(const mmpc_handle* h, int64_t B) {
+    const mmpc_model_info& mi = h->info;
+    if (h->opts.kkt_solver != MMPC_KKT_AUTO) return h->opts.kkt_solver;
+    // measured on one MI355X: condensed when it fits; for the 2-link arm 16 lanes per instance
+    // while one lane per instance would leave most SIMDs idle (B <= 8192); otherwise one lane per instance
+    // (the exo model's 12x12 serial recursion is faster lane-per-instance even at B = 4096)
+    const bool two_link = mi.model_id == MMPC_MODEL_TWO_LINK_ARM;
+    if (two_link && mi.num_shooting_nodes * TwoLinkArm::NU <= 64 && !h->opts.factor_fp32) return MMPC_KKT_CONDENSED;
+    if (two_link && !h->opts.factor_fp32 && B <= 8192 && group_lds_bytes(mi) <= kMaxGroupLds)
+        return MMPC_KKT_RICCATI_GROUP;
+    return MMPC_KKT_RICCATI;
+}
+
 template <class Model, bool BOUNDED>
 int launch_group(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const SolveParams& p, GroupWork gwk) {
     int rc = set_dynamic_lds(sqp_group_kernel<Model, BOUNDED>, lds);
@@ -439,18 +453,8 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
     // points pass NULL for bounds that are all infinite
     const bool bounded = u_lb || u_ub;
-    int solver = h->opts.kkt_solver;
+    const int solver = resolve_kkt_solver(h, B);
     const bool condensed_ok = mi.model_id == MMPC_MODEL_TWO_LINK_ARM && N * TwoLinkArm::NU <= 64;
-    if (solver == MMPC_KKT_AUTO) {
-        // measured on one MI355X: condensed when it fits; for the 2-link arm 16 lanes per instance
-        // while one lane per instance would leave most SIMDs idle (B <= 8192); otherwise one lane per instance
-        // (the exo model's 12x12 serial recursion is faster lane-per-instance even at B = 4096)
-        if (condensed_ok && !h->opts.factor_fp32) solver = MMPC_KKT_CONDENSED;
-        else if (!h->opts.factor_fp32 && mi.model_id == MMPC_MODEL_TWO_LINK_ARM && B <= 8192 &&
-                 group_lds_bytes(mi) <= kMaxGroupLds)
-            solver = MMPC_KKT_RICCATI_GROUP;
-        else solver = MMPC_KKT_RICCATI;
-    }
     if (solver == MMPC_KKT_RICCATI_GROUP) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 needs the lane Riccati solver");
         const size_t lds = group_lds_bytes(mi);
@@ -677,6 +681,12 @@ int mmpc_solve_batch_host(mmpc_handle* h, int64_t B, const double* x0, const dou
     if (iters) MMPC_HIP(hipMemcpyAsync(iters, dit, B * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     if (kkt_res) MMPC_HIP(hipMemcpyAsync(kkt_res, d + off_kkt, B * sizeof(double), hipMemcpyDeviceToHost, s));
     MMPC_HIP(hipStreamSynchronize(s));
+    return MMPC_OK;
+}
+
+int mmpc_resolve_kkt_solver(const mmpc_handle* h, int64_t B, int32_t* solver) {
+    if (!h || !solver || B < 0) return fail(MMPC_ERR_INVALID_ARG, "bad argument");
+    *solver = resolve_kkt_solver(h, B);
     return MMPC_OK;
 }
 

@@ -102,6 +102,7 @@ def lib():
         L.mmpc_linearize_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 5
         L.mmpc_nlp_eval_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 3
         L.mmpc_synth_batch.argtypes = [_vp, C.c_uint64, C.c_int64, C.c_int64] + [_vp] * 4
+        L.mmpc_resolve_kkt_solver.argtypes = [_vp, C.c_int64, C.POINTER(C.c_int32)]
         L.mmpc_status_string.argtypes = [C.c_int32]
         L.mmpc_status_string.restype = C.c_char_p
         L.mmpc_last_error.restype = C.c_char_p
@@ -245,6 +246,12 @@ class Solver:
         _check(lib().mmpc_solve_batch_host(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights), ws,
                                            _ptr(lb), _ptr(ub), _ptr(V), _ptr(st), _ptr(it), _ptr(kkt)))
         return dict(V=V, status=st, iters=it, kkt=kkt)
+
+    def kkt_solver_for(self, B: int) -> int:
+        """KKT_* solver a solve of B instances runs (the AUTO choice resolved)."""
+        v = C.c_int32()
+        _check(lib().mmpc_resolve_kkt_solver(self._h, B, C.byref(v)))
+        return v.value
 
     def linearize_host(self, x, u):
         nx, nu = self.nx, self.nu

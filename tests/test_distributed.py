@@ -69,3 +69,97 @@ def test_shard_arithmetic():
         assert all(parts[i][0] + parts[i][1] == parts[i + 1][0] for i in range(W - 1))
     with pytest.raises(ValueError):
         mdist.shard(-1, 0)
+
+
+class _OracleShardSolver:
+    """test stand-in for mmpc.Solver on CPU tensors: solve_batch through the oracle (the C restatement), so
+    the scatter / broadcast / gather plumbing of mmpc.dist.solve_rank0_batch runs on gloo without a GPU"""
+
+    def __init__(self, N):
+        self.nx, self.nu, self.N, self.NV = 4, 2, N, 6 * N + 4
+
+    def solve_batch(self, B, x0, u_prev, traj, weights, V, status, iters, kkt, weights_stride=0, u_lb=None,
+                    u_ub=None):
+        import oracle_lib
+        r = oracle_lib.solve_batch(self.N, 0.002, x0.numpy(), u_prev.numpy(), traj.numpy(),
+                                   weights.numpy().reshape(B, -1) if weights_stride else weights.numpy(),
+                                   V=V.numpy(), u_lb=None if u_lb is None else u_lb.numpy(),
+                                   u_ub=None if u_ub is None else u_ub.numpy(), nthreads=1)
+        V.copy_(__import__("torch").from_numpy(r["V"]))
+        status.copy_(__import__("torch").from_numpy(r["status"]))
+        iters.copy_(__import__("torch").from_numpy(r["iters"]))
+        kkt.copy_(__import__("torch").from_numpy(r["kkt"]))
+
+
+def _rank0_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "mahi-mpc_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    import oracle_lib
+    from mmpc import dist as mdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, B = 30, 37
+    solver = _OracleShardSolver(N)
+    out = []
+    for case in range(2):
+        if rank == 0:
+            x0, up, tr = (torch.from_numpy(a) for a in oracle_lib.synth(11, 0, B, N, 0.002))
+            if case == 0:   # shared weights, bounds, cold start
+                kw = dict(weights=torch.tensor(WEIGHTS_CFG, dtype=torch.float64),
+                          u_lb=torch.tensor([-3.0, -2.0], dtype=torch.float64),
+                          u_ub=torch.tensor([2.0, 3.0], dtype=torch.float64))
+            else:           # per-instance weights, warm start
+                w = np.tile(WEIGHTS_CFG, (B, 1)) * np.linspace(0.5, 2.0, B)[:, None]
+                kw = dict(weights=torch.from_numpy(w), weights_stride=8,
+                          V=torch.full((B, 6 * N + 4), 0.1, dtype=torch.float64))
+            r = mdist.solve_rank0_batch(solver, x0, up, tr, **kw)
+        else:
+            r = mdist.solve_rank0_batch(solver)
+        out.append(None if r is None else {k: v.numpy().copy() for k, v in r.items()})
+    # ResultGather: weak-scaled per-step results to rank 0
+    Bw = 5
+    g = mdist.ResultGather(Bw, 4, 2)
+    for step in range(2):
+        V = torch.arange(Bw * 10, dtype=torch.float64).reshape(Bw, 10) + 1000 * rank + 100 * step
+        g.post(V, torch.full((Bw,), rank, dtype=torch.int32), torch.full((Bw,), step, dtype=torch.int32))
+    g.wait()
+    last = g.last().numpy().copy()
+    if rank == 0:
+        q.put((out, last))
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank0_batch_scatter_solve_gather(world, oracle):
+    """a rank-0 batch is scattered in contiguous shards (37 instances over 2 / 3 ranks, ragged),
+    weights/bounds broadcast, results gathered -- equal to the single-process solve bit for bit"""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank0_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out, last = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    N, B = 30, 37
+    x0, up, tr = oracle.synth(11, 0, B, N, 0.002)
+    ref0 = oracle.solve_batch(N, 0.002, x0, up, tr, np.array(WEIGHTS_CFG), u_lb=[-3.0, -2.0], u_ub=[2.0, 3.0])
+    w = np.tile(WEIGHTS_CFG, (B, 1)) * np.linspace(0.5, 2.0, B)[:, None]
+    ref1 = oracle.solve_batch(N, 0.002, x0, up, tr, w, V=np.full((B, 6 * N + 4), 0.1))
+    for got, ref in ((out[0], ref0), (out[1], ref1)):
+        np.testing.assert_array_equal(got["V"], ref["V"])
+        np.testing.assert_array_equal(got["status"], ref["status"])
+        np.testing.assert_array_equal(got["iters"], ref["iters"])
+    # ResultGather: rank-major rows of (u_0*, status, iters) of the last step
+    assert last.shape == (world * 5, 4)
+    for r in range(world):
+        rows = last[r * 5:(r + 1) * 5]
+        np.testing.assert_array_equal(rows[:, :2], (np.arange(50).reshape(5, 10) + 1000 * r + 100)[:, 4:6])
+        assert (rows[:, 2] == r).all() and (rows[:, 3] == 1).all()

@@ -170,3 +170,20 @@ def test_bounded_cfg3_batch_properties(mmpc_mod, oracle, tmp_path):
         g = oracle.reduced_gradient(N, H, x0n[b], U[b], upn[b], trn[b], W_EXO, model=oracle.EXO).reshape(-1)
         u = U[b].reshape(-1)
         assert np.abs(u - np.clip(u - g, np.tile(lbn, N), np.tile(ubn, N))).max() <= 1e-7
+
+
+def test_rank0_batch_api_single_process(mmpc_mod, oracle, tmp_path):
+    """mmpc.dist.solve_rank0_batch on one GPU without a process group (the N>1 plumbing is tested on gloo in
+    tests/test_distributed.py): same result as the host API"""
+    import torch
+    from mmpc import dist as mdist
+    N, B = 30, 100
+    x0, up, tr = oracle.synth(21, 0, B, N, H)
+    s = _solver(tmp_path, mmpc_mod, "two_link_arm", N, mmpc_mod.KKT_AUTO)
+    f = dict(dtype=torch.float64, device="cuda")
+    r = mdist.solve_rank0_batch(s, torch.tensor(x0, **f), torch.tensor(up, **f), torch.tensor(tr, **f),
+                                weights=torch.tensor(WEIGHTS_CFG, **f), u_lb=torch.tensor([-2.0, -2.0], **f),
+                                u_ub=torch.tensor([2.0, 2.0], **f), device="cuda")
+    h = s.solve_batch_host(x0, up, tr, np.array(WEIGHTS_CFG), u_lb=[-2.0, -2.0], u_ub=[2.0, 2.0])
+    np.testing.assert_array_equal(r["V"].cpu().numpy(), h["V"])
+    np.testing.assert_array_equal(r["status"].cpu().numpy(), h["status"])
