@@ -6,7 +6,7 @@ OUT=${OUT:-gpurun_out/r01}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 echo "== rocminfo gfx" && (rocminfo 2>/dev/null | grep -m1 -o "gfx9[0-9a-z]*" || true)
-timeout -k 10 600 python -m pytest tests -q -m gpu > "$OUT/pytest_gpu.log" 2>&1; rc=$?
+timeout -k 10 900 python -m pytest tests -q -m gpu > "$OUT/pytest_gpu.log" 2>&1; rc=$?
 tail -30 "$OUT/pytest_gpu.log"
 [ $rc -eq 0 ] || { echo "pytest gpu failed rc=$rc"; exit $rc; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { cat "$OUT/smoke.log"; exit 1; }
