@@ -25,7 +25,8 @@ constexpr int kGroupsPerWave = 4;
 
 // LDS doubles per instance
 __host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int N) {
-    return N * (3 * nx + 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + 3 * nu) + 3 * (N + 1) * nx;
+    return N * (3 * nx + 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + 3 * nu) + 3 * (N + 1) * nx +
+           2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + nx;  // + linear-mode block
 }
 // HBM workspace doubles per instance: K_k | kff_k per stage
 __host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) { return N * nu * (nx + nu + 1); }
@@ -117,6 +118,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const sFu = sFqd + N * NQ * NQ;                        // [N][NQ*NU]   h dacc/du
     double* const sR = sFu + N * NQ * NU;                          // [N][NX]      targets r_k
     double* const sHold = sR + N * NX;                             // [N][NU]      bound a control is held at
+    double* const sLin = sHold + N * NU;                           // linear mode: Fq | Fqd | Fu | xdot
     double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
     const double* const trg = p.traj + ii * (int64_t)N * NX;
 
@@ -148,20 +150,33 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         }
     }
     const double* const tr = sR;
-    // linear mode: acceleration Jacobians and xdot at (x_0, u_prev) (ModelControl.cpp:125-135), in registers
+    // linear mode: acceleration Jacobians and xdot at (x_0, u_prev) (ModelControl.cpp:125-135), in LDS (keeps
+    // 20-64 VGPRs free for the serial Riccati sweep); the linearisation point x_0 is sX[0..NX) (pinned)
     const bool lin = p.is_linear != 0;
-    double lFq[NQ * NQ], lFqd[NQ * NQ], lFu[NQ * NU], lxd[NX], lxs[NX];
-    if (lin) {
-        double acc[NQ];
+    double* const lFq = sLin;
+    double* const lFqd = lFq + NQ * NQ;
+    double* const lFu = lFqd + NQ * NQ;
+    double* const lxd = lFu + NQ * NU;
+    const double* const lxs = sX;
+    if (lin && gl == 0) {
+        double acc[NQ], x[NX], Fq[NQ * NQ], Fqd[NQ * NQ], Fu[NQ * NU];
 #pragma unroll
-        for (int r = 0; r < NX; ++r) lxs[r] = p.x0[ii * NX + r];
-        Model::eval_acc_jac(lxs, up, acc, lFq, lFqd, lFu);
+        for (int r = 0; r < NX; ++r) x[r] = p.x0[ii * NX + r];
+        Model::eval_acc_jac(x, up, acc, Fq, Fqd, Fu);
+#pragma unroll
+        for (int i = 0; i < NQ * NQ; ++i) {
+            lFq[i] = Fq[i];
+            lFqd[i] = Fqd[i];
+        }
+#pragma unroll
+        for (int i = 0; i < NQ * NU; ++i) lFu[i] = Fu[i];
 #pragma unroll
         for (int i = 0; i < NQ; ++i) {
-            lxd[i] = lxs[NQ + i];
+            lxd[i] = x[NQ + i];
             lxd[NQ + i] = acc[i];
         }
     }
+    __builtin_amdgcn_wave_barrier();
     int status = ST_MAX_ITER;
     int it = 0;
     double kkt = 0.0, mu = 0.0, pg_prev = INFINITY;
@@ -397,35 +412,48 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                     for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
                 }
-                double Ld[NU][NU], il[NU];
-#pragma unroll
-                for (int a = 0; a < NU; ++a) {
-                    double sd = Hww[a][a];
-#pragma unroll
-                    for (int q = 0; q < a; ++q) sd = fma(-Ld[a][q], Ld[a][q], sd);
-                    fact_ok &= (sd > 0.0) && isfinite(sd);
-                    const double lj = sqrt(fmax(sd, 1e-300));
-                    Ld[a][a] = lj;
-                    il[a] = 1.0 / lj;
-#pragma unroll
-                    for (int b = a + 1; b < NU; ++b) {
-                        double t = Hww[a][b];
-#pragma unroll
-                        for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
-                        Ld[b][a] = t * il[a];
-                    }
-                }
-#pragma unroll
-                for (int a = 0; a < NU; ++a)
+                // [K_k | kff_k] = -H_ww^-1 [H_wx | -R | h_w] (into wK) and Y with Y^T Y = Z^T H_ww^-1 Z for the
+                // update of P~ and p~.  nu = 2: explicit inverse (one reciprocal; no square roots -- the serial
+                // sweep is latency-bound); otherwise Cholesky, Y = L^-1 Z.
+                double Kt[NU][NS + 1];
+                if constexpr (NU == 2) {
+                    const double det = fma(Hww[0][0], Hww[1][1], -Hww[0][1] * Hww[0][1]);
+                    fact_ok &= (Hww[0][0] > 0.0) && (det > 0.0) && isfinite(det);
+                    const double idet = 1.0 / det;
+                    const double i00 = Hww[1][1] * idet, i11 = Hww[0][0] * idet, i01 = -Hww[0][1] * idet;
 #pragma unroll
                     for (int j = 0; j <= NS; ++j) {
-                        double t = Y[a][j];
-#pragma unroll
-                        for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
-                        Y[a][j] = t * il[a];
+                        Kt[0][j] = fma(i00, Y[0][j], i01 * Y[1][j]);
+                        Kt[1][j] = fma(i01, Y[0][j], i11 * Y[1][j]);
                     }
-                {
-                    double Kt[NU][NS + 1];
+                } else {
+                    double Ld[NU][NU], il[NU];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        double sd = Hww[a][a];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) sd = fma(-Ld[a][q], Ld[a][q], sd);
+                        fact_ok &= (sd > 0.0) && isfinite(sd);
+                        const double lj = sqrt(fmax(sd, 1e-300));
+                        Ld[a][a] = lj;
+                        il[a] = 1.0 / lj;
+#pragma unroll
+                        for (int b = a + 1; b < NU; ++b) {
+                            double t = Hww[a][b];
+#pragma unroll
+                            for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
+                            Ld[b][a] = t * il[a];
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < NU; ++a)
+#pragma unroll
+                        for (int j = 0; j <= NS; ++j) {
+                            double t = Y[a][j];
+#pragma unroll
+                            for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
+                            Y[a][j] = t * il[a];
+                        }
 #pragma unroll
                     for (int a = NU - 1; a >= 0; --a)
 #pragma unroll
@@ -435,24 +463,27 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                             for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], Kt[q][j], t);
                             Kt[a][j] = t * il[a];
                         }
-#pragma unroll
-                    for (int a = 0; a < NU; ++a)
-#pragma unroll
-                        for (int j = 0; j <= NS; ++j) wK[(k * NU + a) * (NS + 1) + j] = -Kt[a][j];
                 }
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int j = 0; j <= NS; ++j) wK[(k * NU + a) * (NS + 1) + j] = -Kt[a][j];
                 if (k == 0) break;
+                // P~_k = blkdiag(A^T P_xx A + Q, R) - Z^T H_ww^-1 Z, p~_k = pn - Z^T H_ww^-1 h_w:
+                // nu = 2 as Y^T Kt (Y = Z, Kt = H_ww^-1 Z), Cholesky as Y^T Y (Y = L^-1 Z)
+                const double(&YB)[NU][NS + 1] = (NU == 2) ? Kt : Y;
 #pragma unroll
                 for (int a = 0; a < NS; ++a) {
                     double t = pn[a];
 #pragma unroll
-                    for (int q = 0; q < NU; ++q) t = fma(-Y[q][a], Y[q][NS], t);
+                    for (int q = 0; q < NU; ++q) t = fma(-Y[q][a], YB[q][NS], t);
                     if (BOUNDED) t += pex[a];
                     pv[a] = t;
 #pragma unroll
                     for (int b = a; b < NS; ++b) {
                         double v = (b < NX) ? Pn[a][b] : ((a == b) ? R[a - NX] : 0.0);
 #pragma unroll
-                        for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
+                        for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], YB[q][b], v);
                         P[a][b] = v;
                     }
                 }
