@@ -419,7 +419,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 if constexpr (NU == 2) {
                     const double det = fma(Hww[0][0], Hww[1][1], -Hww[0][1] * Hww[0][1]);
                     fact_ok &= (Hww[0][0] > 0.0) && (det > 0.0) && isfinite(det);
-                    const double idet = 1.0 / det;
+                    const double idet = rcp_nr(det);  // two Newton steps: ~1 ulp, off the division's long chain
                     const double i00 = Hww[1][1] * idet, i11 = Hww[0][0] * idet, i01 = -Hww[0][1] * idet;
 #pragma unroll
                     for (int j = 0; j <= NS; ++j) {
@@ -434,9 +434,13 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                         for (int q = 0; q < a; ++q) sd = fma(-Ld[a][q], Ld[a][q], sd);
                         fact_ok &= (sd > 0.0) && isfinite(sd);
-                        const double lj = sqrt(fmax(sd, 1e-300));
-                        Ld[a][a] = lj;
-                        il[a] = 1.0 / lj;
+                        // 1/sqrt by v_rsq + two Newton steps (no square root and division on the serial chain)
+                        const double sp = fmax(sd, 1e-300);
+                        double r = __builtin_amdgcn_rsq(sp);
+                        r = r * fma(-0.5 * sp * r, r, 1.5);
+                        r = r * fma(-0.5 * sp * r, r, 1.5);
+                        Ld[a][a] = sp * r;
+                        il[a] = r;
 #pragma unroll
                         for (int b = a + 1; b < NU; ++b) {
                             double t = Hww[a][b];
@@ -526,6 +530,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             _Pragma("unroll") for (int c_ = 0; c_ < NU; ++c_) nu_[c_] = sU[kk_ * NU + c_];             \
         } while (0)
             GROUP_LOAD_STEP(0);
+            // unrolled by two so that the prefetch buffers are renamed instead of copied (2-link only: the exo
+            // step spills when unrolled)
+            constexpr int kStepUnroll = NX <= 4 ? 2 : 1;
+#pragma unroll kStepUnroll
             for (int k = 0; k < N; ++k) {
                 double K[NK], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU], Fk[NX], ck[NX], rk[NX], uk[NU];
 #pragma unroll
@@ -598,12 +606,38 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     d[r] = 0.0;
                     sD[r] = 0.0;
                 }
+                // the operands of step k+1 are loaded during step k (the recursion is latency-bound)
+                double aq[NQ * NQ], ad[NQ * NQ], ac[NX];
+#pragma unroll
+                for (int i = 0; i < NQ * NQ; ++i) {
+                    aq[i] = sFq[i];
+                    ad[i] = sFqd[i];
+                }
+#pragma unroll
+                for (int r = 0; r < NX; ++r) ac[r] = sC[r];
+                constexpr int kDUnroll = NX <= 4 ? 2 : 1;
+#pragma unroll kDUnroll
                 for (int k = 0; k < N; ++k) {
-                    double dn[NX];
-                    a_mul<NQ, double>(h, sFq + k * NQ * NQ, sFqd + k * NQ * NQ, d, dn);
+                    double fq[NQ * NQ], fd[NQ * NQ], cc[NX], dn[NX];
+#pragma unroll
+                    for (int i = 0; i < NQ * NQ; ++i) {
+                        fq[i] = aq[i];
+                        fd[i] = ad[i];
+                    }
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) cc[r] = ac[r];
+                    const int kn = k + 1 < N ? k + 1 : k;
+#pragma unroll
+                    for (int i = 0; i < NQ * NQ; ++i) {
+                        aq[i] = sFq[kn * NQ * NQ + i];
+                        ad[i] = sFqd[kn * NQ * NQ + i];
+                    }
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) ac[r] = sC[kn * NX + r];
+                    a_mul<NQ, double>(h, fq, fd, d, dn);
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
-                        d[r] = dn[r] + sC[k * NX + r];
+                        d[r] = dn[r] + cc[r];
                         sD[(k + 1) * NX + r] = d[r];
                     }
                 }
