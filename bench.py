@@ -174,14 +174,16 @@ def main():
     total = B * world * args.steps
     value = total / elapsed
     # algorithmic flops of one launch = per-iteration figure x the SQP iterations the launch's instances
-    # actually took (unit of work = 1 solve = sum over its iterations).  Condensed kernel: the SURVEY.md 8(d)
-    # figure.  Riccati kernel: its own algorithmic count -- 8(d)'s figure prices the condensed algorithm
-    # (9.3 MFLOP/iter at cfg#3) and would overstate the achieved rate ~45x (reported alongside).
+    # actually took (unit of work = 1 solve = sum over its iterations), SURVEY.md 8(d)'s figure whichever KKT
+    # solver ran -- except where that figure (which prices the condensed algorithm: 9.3 MFLOP/iter at cfg#3)
+    # would put a Riccati kernel above the FP64 peak; there the kernel's own algorithmic count is used
+    # (both are reported).
     survey_fl = float(iters.sum()) * mmpc.survey_flops_per_iteration(N, nx, nu)
+    survey_tf = survey_fl / (kern_ms * 1e-3) / 1e12
     if riccati:
         fl = mmpc.riccati_flops_per_iteration(N, nx, nu)
         own_fl = float(iters.sum()) * fl["total"]
-        achieved = own_fl / (kern_ms * 1e-3) / 1e12
+        achieved = survey_tf if survey_tf <= FP64_PEAK_TFLOPS else own_fl / (kern_ms * 1e-3) / 1e12
         kname = (f"sqp_{'group' if ksolver == 3 else 'lane'}_kernel<"
                  f"{'ExoArm' if cfg['model'] == 'exo_arm' else 'TwoLinkArm'}>")
     else:
@@ -192,7 +194,7 @@ def main():
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
-            tj = json.load(open(args.traffic_json)).get(args.config, {})
+            tj = json.load(open(args.traffic_json)).get(f"{args.config}:{kname}", {})
             if tj.get("batch") == B and tj.get("horizon") == N:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:

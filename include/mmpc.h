@@ -93,8 +93,9 @@ enum mmpc_model_id {
 
 /* KKT solve of each SQP iteration (both solve the same Gauss-Newton QP exactly) */
 enum mmpc_kkt_solver {
-    MMPC_KKT_AUTO = 0,      /* 2-link arm: condensed when N*nu <= 64, else the 16-lane Riccati solver for
-                               B <= 8192 when its LDS fits; otherwise one lane per instance */
+    MMPC_KKT_AUTO = 0,      /* by shape and batch: 2-link arm -- CONDENSED for N*nu <= 64 and
+                               B <= 2560, RICCATI_GROUP up to B*N = 1e6, else RICCATI; exo -- RICCATI_GROUP
+                               for B <= 4096 when two workgroups fit a CU's LDS, else RICCATI */
     MMPC_KKT_CONDENSED = 1, /* one wavefront per instance, condensed Hessian row per lane (N*nu <= 64) */
     MMPC_KKT_RICCATI = 2,   /* one lane per instance, Riccati recursion, any N (needs a workspace) */
     MMPC_KKT_RICCATI_GROUP = 3 /* 16 lanes per instance: stage-parallel model evaluations and line search,

@@ -355,8 +355,9 @@ size_t group_workspace_bytes(const mmpc_model_info& mi, int64_t B) {
     return static_cast<size_t>(group_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) *
            static_cast<size_t>(B) * sizeof(double);
 }
-size_t group_lds_bytes(const mmpc_model_info& mi) {
-    return static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) * kGroupsPerWave *
+size_t group_lds_bytes(const mmpc_model_info& mi, bool bounded = true) {
+    return static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes, bounded,
+                                                 mi.is_linear != 0)) * kGroupsPerWave *
            sizeof(double);
 }
 constexpr size_t kMaxGroupLds = 160 * 1024;  // gfx950: 160 KB of LDS per workgroup (attribute raised above 64 KB)
@@ -373,13 +374,18 @@ int set_dynamic_lds(K kernel, size_t bytes) {
 int resolve_kkt_solver(const mmpc_handle* h, int64_t B) {
     const mmpc_model_info& mi = h->info;
     if (h->opts.kkt_solver != MMPC_KKT_AUTO) return h->opts.kkt_solver;
-    // measured on one MI355X: condensed when it fits; for the 2-link arm 16 lanes per instance
-    // while one lane per instance would leave most SIMDs idle (B <= 8192); otherwise one lane per instance
-    // (the exo model's 12x12 serial recursion is faster lane-per-instance even at B = 4096)
-    const bool two_link = mi.model_id == MMPC_MODEL_TWO_LINK_ARM;
-    if (two_link && mi.num_shooting_nodes * TwoLinkArm::NU <= 64 && !h->opts.factor_fp32) return MMPC_KKT_CONDENSED;
-    if (two_link && !h->opts.factor_fp32 && B <= 8192 && group_lds_bytes(mi) <= kMaxGroupLds)
-        return MMPC_KKT_RICCATI_GROUP;
+    if (h->opts.factor_fp32) return MMPC_KKT_RICCATI;
+    // measured on one MI355X (tools/solver_sweep.py): 2-link arm -- condensed for small batches
+    // (B <= 2560 at N*nu <= 64), the 16-lane Riccati kernel up to B*N = 1e6, one lane per instance beyond;
+    // exo -- the 16-lane kernel while at least two of its workgroups fit a CU's LDS and B <= 4096
+    const int N = mi.num_shooting_nodes;
+    const size_t glds = group_lds_bytes(mi, true);  // with the bounded solves' hold targets (the larger layout)
+    if (mi.model_id == MMPC_MODEL_TWO_LINK_ARM) {
+        if (N * TwoLinkArm::NU <= 64 && B <= 2560) return MMPC_KKT_CONDENSED;
+        if (glds <= kMaxGroupLds && B * static_cast<int64_t>(N) <= 1000000) return MMPC_KKT_RICCATI_GROUP;
+        return MMPC_KKT_RICCATI;
+    }
+    if (glds <= kMaxGroupLds / 2 && B <= 4096) return MMPC_KKT_RICCATI_GROUP;
     return MMPC_KKT_RICCATI;
 }
 
@@ -419,6 +425,8 @@ int ensure_workspace(mmpc_handle* h, int64_t B, LaneWork* lw) {
     return ensure_workspace_bytes(h, std::max(workspace_bytes(h->info, B), group_workspace_bytes(h->info, B)), &lw->ws);
 }
 
+int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded, hipStream_t stream);
+
 int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
                  const double* weights, int64_t w_stride, const double* u_lb, const double* u_ub, double* V,
                  int32_t* status, int32_t* iters, double* kkt, hipStream_t stream, double* trace = nullptr) {
@@ -449,15 +457,22 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.iters = iters;
     p.kkt = kkt;
     p.trace = trace;
-    const int N = mi.num_shooting_nodes;
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
     // points pass NULL for bounds that are all infinite
     const bool bounded = u_lb || u_ub;
     const int solver = resolve_kkt_solver(h, B);
+    return launch_kernel(h, solver, p, bounded, stream);
+}
+
+// one kernel launch for solver (not AUTO) on p.B instances
+int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded, hipStream_t stream) {
+    const mmpc_model_info& mi = h->info;
+    const int64_t B = p.B;
+    const int N = mi.num_shooting_nodes;
     const bool condensed_ok = mi.model_id == MMPC_MODEL_TWO_LINK_ARM && N * TwoLinkArm::NU <= 64;
     if (solver == MMPC_KKT_RICCATI_GROUP) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 needs the lane Riccati solver");
-        const size_t lds = group_lds_bytes(mi);
+        const size_t lds = group_lds_bytes(mi, bounded);
         if (lds > kMaxGroupLds) return fail(MMPC_ERR_UNSUPPORTED, "group Riccati solver: stage data exceeds 160 KB LDS");
         LaneWork lw;
         int rc = ensure_workspace(h, B, &lw);

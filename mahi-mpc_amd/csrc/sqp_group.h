@@ -23,10 +23,12 @@ namespace mmpc {
 constexpr int kGroupLanes = 16;
 constexpr int kGroupsPerWave = 4;
 
-// LDS doubles per instance
-__host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int N) {
-    return N * (3 * nx + 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + 3 * nu) + 3 * (N + 1) * nx +
-           2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + nx;  // + linear-mode block
+// LDS doubles per instance.  The hold targets (bounded solves) and the linear-mode block are only allocated
+// when used: at cfg#2 that keeps a 4-instance workgroup at 38.8 KB, so 4 workgroups (one per SIMD) fit a CU's
+// 160 KB; with them 41 KB leaves one SIMD of every CU idle (measured: 0.78 vs 0.6x ms).
+__host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int N, bool bounded = true, bool linear = true) {
+    return N * (3 * nx + 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + 2 * nu) + 3 * (N + 1) * nx +
+           (bounded ? N * nu : 0) + (linear ? 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + nx : 0);
 }
 // HBM workspace doubles per instance: K_k | kff_k per stage
 __host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) { return N * nu * (nx + nu + 1); }
@@ -106,7 +108,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     const double h = p.h;
 
     // ---- LDS views of this instance ----
-    double* const sX = shm + gi * group_lds_doubles(NX, NU, N);  // [N+1][NX]
+    double* const sX = shm + gi * group_lds_doubles(NX, NU, N, BOUNDED, p.is_linear != 0);  // [N+1][NX]
     double* const sDX = sX + (N + 1) * NX;                         // [N+1][NX]
     double* const sD = sDX + (N + 1) * NX;                         // [N+1][NX]
     double* const sU = sD + (N + 1) * NX;                          // [N][NU]
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const sFu = sFqd + N * NQ * NQ;                        // [N][NQ*NU]   h dacc/du
     double* const sR = sFu + N * NQ * NU;                          // [N][NX]      targets r_k
     double* const sHold = sR + N * NX;                             // [N][NU]      bound a control is held at
-    double* const sLin = sHold + N * NU;                           // linear mode: Fq | Fqd | Fu | xdot
+    double* const sLin = sHold + (BOUNDED ? N * NU : 0);           // linear mode: Fq | Fqd | Fu | xdot
     double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
     const double* const trg = p.traj + ii * (int64_t)N * NX;
 

@@ -108,6 +108,24 @@ def test_workspace_size_and_solver_choice(tmp_path, model_json, mmpc_mod):
         mmpc_mod.Solver(p, kkt_solver=7)
 
 
+def test_auto_solver_policy(tmp_path, model_json, mmpc_mod):
+    """MMPC_KKT_AUTO (include/mmpc.h), resolved without a GPU"""
+    m = mmpc_mod
+    s = m.Solver(model_json(N=30))                              # cfg#2 shape
+    assert s.kkt_solver_for(4096) == m.KKT_RICCATI_GROUP and s.kkt_solver_for(2560) == m.KKT_CONDENSED
+    assert s.kkt_solver_for(1) == m.KKT_CONDENSED and s.kkt_solver_for(65536) == m.KKT_RICCATI
+    s = m.Solver(model_json(N=60))                              # N*nu > 64
+    assert s.kkt_solver_for(64) == m.KKT_RICCATI_GROUP and s.kkt_solver_for(16384) == m.KKT_RICCATI_GROUP
+    assert s.kkt_solver_for(16667) == m.KKT_RICCATI
+    assert m.Solver(model_json(N=30), factor_fp32=1).kkt_solver_for(4096) == m.KKT_RICCATI
+    p = m.write_model_json(str(tmp_path / "exo.json"), "exo", 8, 4, 2000, 50, model="exo_arm")
+    assert m.Solver(p).kkt_solver_for(65536) == m.KKT_RICCATI and m.Solver(p).kkt_solver_for(64) == m.KKT_RICCATI
+    p = m.write_model_json(str(tmp_path / "exo20.json"), "exo20", 8, 4, 2000, 20, model="exo_arm")
+    assert m.Solver(p).kkt_solver_for(4096) == m.KKT_RICCATI_GROUP and m.Solver(p).kkt_solver_for(8192) == m.KKT_RICCATI
+    for k in (m.KKT_CONDENSED, m.KKT_RICCATI, m.KKT_RICCATI_GROUP):
+        assert m.Solver(model_json(N=30), kkt_solver=k).kkt_solver_for(4096) == k
+
+
 def test_invalid_opts_rejected(model_json, mmpc_mod):
     with pytest.raises(mmpc_mod.MmpcError):
         mmpc_mod.Solver(model_json(), tol_grad=0.0)
