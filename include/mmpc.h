@@ -87,8 +87,12 @@ enum mmpc_status {
 /* built-in dynamics (device code; see DESIGN.md "Models") */
 enum mmpc_model_id {
     MMPC_MODEL_TWO_LINK_ARM = 0, /* examples/ex_model_generate.cpp:24-43, nx=4 nu=2 */
-    MMPC_MODEL_EXO_ARM = 1       /* 4-DoF exo, nx=8 nu=4: M(q) of src/inverseTest.cpp:59-74 with the
+    MMPC_MODEL_EXO_ARM = 1,      /* 4-DoF exo, nx=8 nu=4: M(q) of src/inverseTest.cpp:59-74 with the
                                     build-defined parameters of tests/golden/exo_params.json */
+    MMPC_MODEL_USER = 2          /* dynamics given as SX expressions to mahi::mpc::ModelGenerator
+                                    (ModelGenerator.hpp:23; examples/ex_model_generate.cpp:36-43), compiled by
+                                    compile_model() into the model's own <name>.so, which exports this same
+                                    C-ABI for that one model (the JSON's dll_filepath, ModelGenerator.cpp:255) */
 };
 
 /* KKT solve of each SQP iteration (both solve the same Gauss-Newton QP exactly) */

@@ -15,6 +15,7 @@
 #include <mutex>
 #include <sstream>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/mmpc.h"
@@ -23,6 +24,16 @@
 #include "sqp_group.h"
 #include "sqp_lane.h"
 #include "sqp_wave.h"
+
+// A library built by ModelGenerator::compile_model for SX-defined dynamics (mahi-mpc's <name>.so,
+// ModelGenerator.cpp:254-259) compiles this same file with -DMMPC_USER_MODEL_HEADER="<name>_model.h", which
+// defines mmpc::UserModel; it then serves that one model (MMPC_MODEL_USER) and none of the built-in ones.
+#ifdef MMPC_USER_MODEL_HEADER
+#include MMPC_USER_MODEL_HEADER
+#define MMPC_BUILTIN_MODELS 0
+#else
+#define MMPC_BUILTIN_MODELS 1
+#endif
 
 using namespace mmpc;
 
@@ -47,6 +58,7 @@ int hip_fail(hipError_t e, const char* where) {
 // ---------------------------------------------------------------- handle
 struct mmpc_handle {
     mmpc_model_info info;
+    int nq = 0;  // kinematic rows of the model's dynamics (sqp_lane.h a_mul)
     mmpc_opts opts;
     std::mutex host_mu;  // serialises the *_host entry points
     hipStream_t host_stream = nullptr;
@@ -146,6 +158,16 @@ int parse_model(const std::string& text, mmpc_model_info* info) {
     if ((rc = bounds("u_max", info->u_max, info->num_u, 10e30, false))) return rc;
     // dynamics: explicit "mmpc_model" key, else the only built-in model with these dimensions
     const json::Value* mdl = m->get("mmpc_model");
+#if !MMPC_BUILTIN_MODELS
+    // a generated library serves exactly its own model
+    if (mdl && mdl->kind == json::Value::String && mdl->str != UserModel::kName)
+        return fail(MMPC_ERR_UNSUPPORTED, "this library was generated for model \"" + std::string(UserModel::kName) +
+                                              "\", not \"" + mdl->str + "\"");
+    if (info->num_x != UserModel::NX || info->num_u != UserModel::NU)
+        return fail(MMPC_ERR_PARSE, "num_x / num_u differ from the generated model's dimensions");
+    info->model_id = MMPC_MODEL_USER;
+    return MMPC_OK;
+#endif
     if (mdl && mdl->kind == json::Value::String) {
         if (mdl->str == "two_link_arm" || mdl->str == "double_pendulum") info->model_id = MMPC_MODEL_TWO_LINK_ARM;
         else if (mdl->str == "exo_arm" || mdl->str == "exo") info->model_id = MMPC_MODEL_EXO_ARM;
@@ -345,9 +367,29 @@ __global__ __launch_bounds__(256) void synth_exo_kernel(uint64_t seed, int64_t f
 
 inline unsigned grid1d(int64_t B, int threads) { return static_cast<unsigned>((B + threads - 1) / threads); }
 
-size_t workspace_bytes(const mmpc_model_info& mi, int64_t B) {
+// Calls f((Model*)nullptr) for the model compiled into this library under model_id.
+template <class F>
+int with_model(int model_id, F&& f) {
+#if MMPC_BUILTIN_MODELS
+    if (model_id == MMPC_MODEL_TWO_LINK_ARM) return f(static_cast<TwoLinkArm*>(nullptr));
+    if (model_id == MMPC_MODEL_EXO_ARM) return f(static_cast<ExoArm*>(nullptr));
+#else
+    if (model_id == MMPC_MODEL_USER) return f(static_cast<UserModel*>(nullptr));
+#endif
+    return fail(MMPC_ERR_UNSUPPORTED, "model not compiled into this library");
+}
+int model_nq(int model_id) {
+    int nq = 0;
+    with_model(model_id, [&](auto* m) {
+        nq = std::remove_pointer_t<decltype(m)>::NQ;
+        return MMPC_OK;
+    });
+    return nq;
+}
+
+size_t workspace_bytes(const mmpc_model_info& mi, int nq, int64_t B) {
     const int64_t blocks = (B + 63) / 64;
-    return static_cast<size_t>(lane_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) * 64u *
+    return static_cast<size_t>(lane_ws_doubles(mi.num_x, mi.num_u, nq, mi.num_shooting_nodes)) * 64u *
            static_cast<size_t>(blocks) * sizeof(double);
 }
 
@@ -355,8 +397,8 @@ size_t group_workspace_bytes(const mmpc_model_info& mi, int64_t B) {
     return static_cast<size_t>(group_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) *
            static_cast<size_t>(B) * sizeof(double);
 }
-size_t group_lds_bytes(const mmpc_model_info& mi, bool bounded = true) {
-    return static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes, bounded,
+size_t group_lds_bytes(const mmpc_model_info& mi, int nq, bool bounded = true) {
+    return static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, nq, mi.num_shooting_nodes, bounded,
                                                  mi.is_linear != 0)) * kGroupsPerWave *
            sizeof(double);
 }
@@ -379,7 +421,11 @@ int resolve_kkt_solver(const mmpc_handle* h, int64_t B) {
     // (B <= 2560 at N*nu <= 64), the 16-lane Riccati kernel up to B*N = 1e6, one lane per instance beyond;
     // exo -- the 16-lane kernel while at least two of its workgroups fit a CU's LDS and B <= 4096
     const int N = mi.num_shooting_nodes;
-    const size_t glds = group_lds_bytes(mi, true);  // with the bounded solves' hold targets (the larger layout)
+    const size_t glds = group_lds_bytes(mi, h->nq, true);  // with the bounded solves' hold targets (larger)
+    if (mi.model_id == MMPC_MODEL_USER) {  // SX-generated dynamics: no condensed kernel (it is 2-link specific)
+        if (glds <= kMaxGroupLds / 2 && B * static_cast<int64_t>(N) <= 1000000) return MMPC_KKT_RICCATI_GROUP;
+        return MMPC_KKT_RICCATI;
+    }
     if (mi.model_id == MMPC_MODEL_TWO_LINK_ARM) {
         if (N * TwoLinkArm::NU <= 64 && B <= 2560) return MMPC_KKT_CONDENSED;
         if (glds <= kMaxGroupLds && B * static_cast<int64_t>(N) <= 1000000) return MMPC_KKT_RICCATI_GROUP;
@@ -422,7 +468,8 @@ int ensure_workspace_bytes(mmpc_handle* h, size_t bytes, double** out) {
     return MMPC_OK;
 }
 int ensure_workspace(mmpc_handle* h, int64_t B, LaneWork* lw) {
-    return ensure_workspace_bytes(h, std::max(workspace_bytes(h->info, B), group_workspace_bytes(h->info, B)), &lw->ws);
+    return ensure_workspace_bytes(h, std::max(workspace_bytes(h->info, h->nq, B), group_workspace_bytes(h->info, B)),
+                                  &lw->ws);
 }
 
 int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded, hipStream_t stream);
@@ -469,30 +516,29 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
     const mmpc_model_info& mi = h->info;
     const int64_t B = p.B;
     const int N = mi.num_shooting_nodes;
-    const bool condensed_ok = mi.model_id == MMPC_MODEL_TWO_LINK_ARM && N * TwoLinkArm::NU <= 64;
     if (solver == MMPC_KKT_RICCATI_GROUP) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 needs the lane Riccati solver");
-        const size_t lds = group_lds_bytes(mi, bounded);
+        const size_t lds = group_lds_bytes(mi, h->nq, bounded);
         if (lds > kMaxGroupLds) return fail(MMPC_ERR_UNSUPPORTED, "group Riccati solver: stage data exceeds 160 KB LDS");
         LaneWork lw;
         int rc = ensure_workspace(h, B, &lw);
         if (rc) return rc;
         GroupWork gwk{lw.ws};
         dim3 grid(grid1d(B, kGroupsPerWave)), block(64);
-        if (mi.model_id == MMPC_MODEL_EXO_ARM)
-            rc = bounded ? launch_group<ExoArm, true>(grid, block, lds, stream, p, gwk)
-                         : launch_group<ExoArm, false>(grid, block, lds, stream, p, gwk);
-        else
-            rc = bounded ? launch_group<TwoLinkArm, true>(grid, block, lds, stream, p, gwk)
-                         : launch_group<TwoLinkArm, false>(grid, block, lds, stream, p, gwk);
+        rc = with_model(mi.model_id, [&](auto* m) {
+            using M = std::remove_pointer_t<decltype(m)>;
+            return bounded ? launch_group<M, true>(grid, block, lds, stream, p, gwk)
+                           : launch_group<M, false>(grid, block, lds, stream, p, gwk);
+        });
         if (rc) return rc;
         MMPC_HIP(hipGetLastError());
         return MMPC_OK;
     }
     if (solver == MMPC_KKT_CONDENSED) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 is a Riccati-solver option");
+#if MMPC_BUILTIN_MODELS
         // host-side shape checks: the kernel holds one condensed-Hessian row per lane
-        if (!condensed_ok)
+        if (mi.model_id != MMPC_MODEL_TWO_LINK_ARM || N * TwoLinkArm::NU > 64)
             return fail(MMPC_ERR_UNSUPPORTED, "condensed solver needs the 2-link arm and N*nu <= 64");
         dim3 grid(static_cast<unsigned>(B)), block(64);
         if (bounded) {
@@ -504,19 +550,22 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
             else if (N <= 30) sqp_wave_kernel<TwoLinkArm, 30><<<grid, block, 0, stream>>>(p);
             else sqp_wave_kernel<TwoLinkArm, 32><<<grid, block, 0, stream>>>(p);
         }
+#else
+        return fail(MMPC_ERR_UNSUPPORTED, "condensed solver needs the built-in 2-link arm");
+#endif
     } else {
         LaneWork lw;
         int rc = ensure_workspace(h, B, &lw);
         if (rc) return rc;
         dim3 grid(grid1d(B, 64)), block(64);
         const bool f32 = h->opts.factor_fp32 != 0;
-        if (mi.model_id == MMPC_MODEL_EXO_ARM) {
-            if (f32) launch_lane<ExoArm, float>(bounded, grid, block, stream, p, lw);
-            else launch_lane<ExoArm, double>(bounded, grid, block, stream, p, lw);
-        } else {
-            if (f32) launch_lane<TwoLinkArm, float>(bounded, grid, block, stream, p, lw);
-            else launch_lane<TwoLinkArm, double>(bounded, grid, block, stream, p, lw);
-        }
+        rc = with_model(mi.model_id, [&](auto* m) {
+            using M = std::remove_pointer_t<decltype(m)>;
+            if (f32) launch_lane<M, float>(bounded, grid, block, stream, p, lw);
+            else launch_lane<M, double>(bounded, grid, block, stream, p, lw);
+            return MMPC_OK;
+        });
+        if (rc) return rc;
     }
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
@@ -572,6 +621,7 @@ int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_han
     mmpc_handle* h = new (std::nothrow) mmpc_handle();
     if (!h) return fail(MMPC_ERR_INVALID_ARG, "out of memory");
     h->info = info;
+    h->nq = model_nq(info.model_id);
     h->opts = o;
     *out = h;
     g_last_error.clear();
@@ -619,7 +669,7 @@ int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts) {
 int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes) {
     if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
     if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
-    const size_t nb = workspace_bytes(h->info, B);
+    const size_t nb = std::max(workspace_bytes(h->info, h->nq, B), group_workspace_bytes(h->info, B));
     if (bytes) *bytes = nb;
     if (B == 0) return MMPC_OK;
     int dev;
@@ -716,12 +766,13 @@ int mmpc_linearize_batch(mmpc_handle* h, int64_t B, const double* x, const doubl
     if (rc) return rc;
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
-    if (h->info.model_id == MMPC_MODEL_EXO_ARM)
-        linearize_kernel<ExoArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+    rc = with_model(h->info.model_id, [&](auto* m) {
+        using M = std::remove_pointer_t<decltype(m)>;
+        linearize_kernel<M><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
             B, x, u, A_colmajor, B_colmajor, xdot);
-    else
-        linearize_kernel<TwoLinkArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-            B, x, u, A_colmajor, B_colmajor, xdot);
+        return MMPC_OK;
+    });
+    if (rc) return rc;
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
 }
@@ -767,14 +818,14 @@ int mmpc_nlp_eval_batch(mmpc_handle* h, int64_t B, const double* V, const double
     if (rc) return rc;
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
-    if (h->info.model_id == MMPC_MODEL_EXO_ARM)
-        nlp_eval_kernel<ExoArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+    rc = with_model(h->info.model_id, [&](auto* m) {
+        using M = std::remove_pointer_t<decltype(m)>;
+        nlp_eval_kernel<M><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
             B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
             weights_stride, J, defect_inf);
-    else
-        nlp_eval_kernel<TwoLinkArm><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-            B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
-            weights_stride, J, defect_inf);
+        return MMPC_OK;
+    });
+    if (rc) return rc;
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
 }
@@ -785,6 +836,8 @@ int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t
     if (B < 0 || first_index < 0) return fail(MMPC_ERR_INVALID_ARG, "negative B / first_index");
     if (B == 0) return MMPC_OK;
     if (!x0 || !u_prev || !traj) return fail(MMPC_ERR_INVALID_ARG, "null output pointer");
+    if (h->info.model_id == MMPC_MODEL_USER)
+        return fail(MMPC_ERR_UNSUPPORTED, "no synthetic-instance recipe for generated models");
     int dev;
     int rc = resolve_device(h, &dev);
     if (rc) return rc;

@@ -26,9 +26,11 @@ constexpr int kGroupsPerWave = 4;
 // LDS doubles per instance.  The hold targets (bounded solves) and the linear-mode block are only allocated
 // when used: at cfg#2 that keeps a 4-instance workgroup at 38.8 KB, so 4 workgroups (one per SIMD) fit a CU's
 // 160 KB; with them 41 KB leaves one SIMD of every CU idle (measured: 0.78 vs 0.6x ms).
-__host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int N, bool bounded = true, bool linear = true) {
-    return N * (3 * nx + 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + 2 * nu) + 3 * (N + 1) * nx +
-           (bounded ? N * nu : 0) + (linear ? 2 * (nx / 2) * (nx / 2) + (nx / 2) * nu + nx : 0);
+// nq = kinematic rows of the model (sqp_lane.h a_mul); the stage blocks are h da/dq, h da/dz, h da/du.
+__host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int nq, int N, bool bounded = true,
+                                                   bool linear = true) {
+    return N * (3 * nx + (nx - nq) * (nq + (nx - nq) + nu) + 2 * nu) + 3 * (N + 1) * nx + (bounded ? N * nu : 0) +
+           (linear ? (nx - nq) * (nq + (nx - nq) + nu) + nx : 0);
 }
 // HBM workspace doubles per instance: K_k | kff_k per stage
 __host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) { return N * nu * (nx + nu + 1); }
@@ -57,7 +59,7 @@ __device__ __forceinline__ void group_model(bool lin, const double* lFq, const d
                                             const double* lxd, const double* lxs, const double* lus, const double* x,
                                             const double* u, double* xd, double* Fq, double* Fqd, double* Fu,
                                             bool jac) {
-    constexpr int NQ = Model::NQ, NU = Model::NU;
+    constexpr int NQ = Model::NQ, NU = Model::NU, NA = Model::NX - NQ;
     if (!lin) {
         if (jac) {
             Model::eval_acc_jac(x, u, xd + NQ, Fq, Fqd, Fu);
@@ -69,30 +71,35 @@ __device__ __forceinline__ void group_model(bool lin, const double* lFq, const d
         return;
     }
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
-        xd[i] = lxd[i] + (x[NQ + i] - lxs[NQ + i]);
+    for (int i = 0; i < NQ; ++i) xd[i] = lxd[i] + (x[NQ + i] - lxs[NQ + i]);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
         double t = lxd[NQ + i];
 #pragma unroll
-        for (int s = 0; s < NQ; ++s)
-            t = fma(lFq[i * NQ + s], x[s] - lxs[s], fma(lFqd[i * NQ + s], x[NQ + s] - lxs[NQ + s], t));
+        for (int s = 0; s < (NQ > NA ? NQ : NA); ++s) {
+            if (s < NA) t = fma(lFqd[i * NA + s], x[NQ + s] - lxs[NQ + s], t);
+            if (s < NQ) t = fma(lFq[i * NQ + s], x[s] - lxs[s], t);
+        }
 #pragma unroll
         for (int c = 0; c < NU; ++c) t = fma(lFu[i * NU + c], u[c] - lus[c], t);
         xd[NQ + i] = t;
     }
     if (jac) {
 #pragma unroll
-        for (int i = 0; i < NQ * NQ; ++i) {
-            Fq[i] = lFq[i];
-            Fqd[i] = lFqd[i];
-        }
+        for (int i = 0; i < NA * NQ; ++i) Fq[i] = lFq[i];
 #pragma unroll
-        for (int i = 0; i < NQ * NU; ++i) Fu[i] = lFu[i];
+        for (int i = 0; i < NA * NA; ++i) Fqd[i] = lFqd[i];
+#pragma unroll
+        for (int i = 0; i < NA * NU; ++i) Fu[i] = lFu[i];
     }
 }
 
 template <class Model, bool BOUNDED = false>
 __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork gw) {
-    constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NS = NX + NU, ND = NX + NU;
+    constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
+    constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)
+    constexpr int FQ = NA * NQ, FD = NA * NA, FU = NA * NU;  // stage block sizes (sqp_lane.h a_mul)
+    static_assert(NQ >= 0 && NA >= NQ, "x = [q; z] with qdot = z[0:NQ]");
     constexpr int G = kGroupLanes;
     extern __shared__ double shm[];
     const int gl = threadIdx.x & (G - 1);
@@ -108,17 +115,17 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     const double h = p.h;
 
     // ---- LDS views of this instance ----
-    double* const sX = shm + gi * group_lds_doubles(NX, NU, N, BOUNDED, p.is_linear != 0);  // [N+1][NX]
+    double* const sX = shm + gi * group_lds_doubles(NX, NU, NQ, N, BOUNDED, p.is_linear != 0);  // [N+1][NX]
     double* const sDX = sX + (N + 1) * NX;                         // [N+1][NX]
     double* const sD = sDX + (N + 1) * NX;                         // [N+1][NX]
     double* const sU = sD + (N + 1) * NX;                          // [N][NU]
     double* const sDU = sU + N * NU;                               // [N][NU]
     double* const sF = sDU + N * NU;                               // [N][NX]
     double* const sC = sF + N * NX;                                // [N][NX]
-    double* const sFq = sC + N * NX;                               // [N][NQ*NQ]   h dacc/dq
-    double* const sFqd = sFq + N * NQ * NQ;                        // [N][NQ*NQ]   h dacc/dqd
-    double* const sFu = sFqd + N * NQ * NQ;                        // [N][NQ*NU]   h dacc/du
-    double* const sR = sFu + N * NQ * NU;                          // [N][NX]      targets r_k
+    double* const sFq = sC + N * NX;                               // [N][NA*NQ]   h da/dq
+    double* const sFqd = sFq + N * FQ;                             // [N][NA*NA]   h da/dz
+    double* const sFu = sFqd + N * FD;                             // [N][NA*NU]   h da/du
+    double* const sR = sFu + N * FU;                               // [N][NX]      targets r_k
     double* const sHold = sR + N * NX;                             // [N][NU]      bound a control is held at
     double* const sLin = sHold + (BOUNDED ? N * NU : 0);           // linear mode: Fq | Fqd | Fu | xdot
     double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
@@ -156,27 +163,25 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     // 20-64 VGPRs free for the serial Riccati sweep); the linearisation point x_0 is sX[0..NX) (pinned)
     const bool lin = p.is_linear != 0;
     double* const lFq = sLin;
-    double* const lFqd = lFq + NQ * NQ;
-    double* const lFu = lFqd + NQ * NQ;
-    double* const lxd = lFu + NQ * NU;
+    double* const lFqd = lFq + FQ;
+    double* const lFu = lFqd + FD;
+    double* const lxd = lFu + FU;
     const double* const lxs = sX;
     if (lin && gl == 0) {
-        double acc[NQ], x[NX], Fq[NQ * NQ], Fqd[NQ * NQ], Fu[NQ * NU];
+        double acc[NA], x[NX], Fq[SQ], Fqd[FD], Fu[FU];
 #pragma unroll
         for (int r = 0; r < NX; ++r) x[r] = p.x0[ii * NX + r];
         Model::eval_acc_jac(x, up, acc, Fq, Fqd, Fu);
 #pragma unroll
-        for (int i = 0; i < NQ * NQ; ++i) {
-            lFq[i] = Fq[i];
-            lFqd[i] = Fqd[i];
-        }
+        for (int i = 0; i < FQ; ++i) lFq[i] = Fq[i];
 #pragma unroll
-        for (int i = 0; i < NQ * NU; ++i) lFu[i] = Fu[i];
+        for (int i = 0; i < FD; ++i) lFqd[i] = Fqd[i];
 #pragma unroll
-        for (int i = 0; i < NQ; ++i) {
-            lxd[i] = x[NQ + i];
-            lxd[NQ + i] = acc[i];
-        }
+        for (int i = 0; i < FU; ++i) lFu[i] = Fu[i];
+#pragma unroll
+        for (int i = 0; i < NQ; ++i) lxd[i] = x[NQ + i];
+#pragma unroll
+        for (int i = 0; i < NA; ++i) lxd[NQ + i] = acc[i];
     }
     __builtin_amdgcn_wave_barrier();
     int status = ST_MAX_ITER;
@@ -190,19 +195,18 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         double J0 = 0.0, c1 = 0.0, cmax = 0.0;
         int nonfinite = 0;
         for (int k = gl; k < N; k += G) {
-            double x[NX], u[NU], xd[NX], Fq[NQ * NQ], Fqd[NQ * NQ], Fu[NQ * NU];
+            double x[NX], u[NU], xd[NX], Fq[SQ], Fqd[FD], Fu[FU];
 #pragma unroll
             for (int r = 0; r < NX; ++r) x[r] = sX[k * NX + r];
 #pragma unroll
             for (int c = 0; c < NU; ++c) u[c] = sU[k * NU + c];
             group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, Fq, Fqd, Fu, true);
 #pragma unroll
-            for (int i = 0; i < NQ * NQ; ++i) {
-                sFq[k * NQ * NQ + i] = h * Fq[i];
-                sFqd[k * NQ * NQ + i] = h * Fqd[i];
-            }
+            for (int i = 0; i < FQ; ++i) sFq[k * FQ + i] = h * Fq[i];
 #pragma unroll
-            for (int i = 0; i < NQ * NU; ++i) sFu[k * NQ * NU + i] = h * Fu[i];
+            for (int i = 0; i < FD; ++i) sFqd[k * FD + i] = h * Fqd[i];
+#pragma unroll
+            for (int i = 0; i < FU; ++i) sFu[k * FU + i] = h * Fu[i];
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 const double F = fma(h, xd[r], x[r]);
@@ -254,11 +258,11 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
             for (int c = 0; c < NU; ++c) unext[c] = 0.0;
             for (int k = N - 1; k >= 0; --k) {
-                const double* hFq = sFq + k * NQ * NQ;
-                const double* hFqd = sFqd + k * NQ * NQ;
-                double hFu[NQ * NU], x[NX], u[NU], um[NU], cc[NX], tg[NU];
+                const double* hFq = sFq + k * FQ;
+                const double* hFqd = sFqd + k * FD;
+                double hFu[FU], x[NX], u[NU], um[NU], cc[NX], tg[NU];
 #pragma unroll
-                for (int i = 0; i < NQ * NU; ++i) hFu[i] = sFu[k * NQ * NU + i];
+                for (int i = 0; i < FU; ++i) hFu[i] = sFu[k * FU + i];
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
                     x[r] = sX[k * NX + r];
@@ -274,7 +278,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 for (int c = 0; c < NU; ++c) {
                     double g = 0.0;
 #pragma unroll
-                    for (int s = 0; s < NQ; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
+                    for (int s = 0; s < NA; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
                     g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
                     if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
                     if (!BOUNDED) {
@@ -296,7 +300,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1},  e_{k-1} = d_k + x_k - r_{k-1}
                 if (k >= 1) {
                     double ln[NX];
-                    at_mul<NQ, double>(h, hFq, hFqd, lam, ln);
+                    at_mul<NQ, NA, double>(h, hFq, hFqd, lam, ln);
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         lam[r] = fma(Q[r], sD[k * NX + r] + x[r] - tr[(k - 1) * NX + r], ln[r]);
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     for (int c = 0; c < NU; ++c) {
                         double t = Ps(r, NX + c);
 #pragma unroll
-                        for (int s = 0; s < NQ; ++s) t = fma(Ps(r, NQ + s), hFu[s * NU + c], t);
+                        for (int s = 0; s < NA; ++s) t = fma(Ps(r, NQ + s), hFu[s * NU + c], t);
                         Gm[r][c] = t;
                     }
                 double mv[NX];
@@ -329,21 +333,21 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     for (int b = a; b < NU; ++b) {
                         double t = Ps(NX + a, NX + b);
 #pragma unroll
-                        for (int s = 0; s < NQ; ++s)
+                        for (int s = 0; s < NA; ++s)
                             t = fma(hFu[s * NU + a], Gm[NQ + s][b], fma(Ps(NQ + s, NX + a), hFu[s * NU + b], t));
                         if (a == b) t += R[a] + Rm[a];
                         Hww[a][b] = t;
                     }
                     double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
 #pragma unroll
-                    for (int s = 0; s < NQ; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
+                    for (int s = 0; s < NA; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
 #pragma unroll
                     for (int r = 0; r < NX; ++r) t = fma(Ps(r, NX + a), cc[r], t);
                     Y[a][NS] = t;
                     double ga[NX];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) ga[r] = Gm[r][a];
-                    at_mul<NQ, double>(h, hFq, hFqd, ga, &Y[a][0]);
+                    at_mul<NQ, NA, double>(h, hFq, hFqd, ga, &Y[a][0]);
 #pragma unroll
                     for (int c = 0; c < NU; ++c) Y[a][NX + c] = (a == c) ? -R[a] : 0.0;
                 }
@@ -395,20 +399,20 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                             if (b < NQ) {
                                 t = Ps(r, b);
 #pragma unroll
-                                for (int s = 0; s < NQ; ++s) t = fma(hFq[s * NQ + b], Ps(r, NQ + s), t);
+                                for (int s = 0; s < NA; ++s) t = fma(hFq[s * NQ + b], Ps(r, NQ + s), t);
                             } else {
-                                t = fma(h, Ps(r, b - NQ), Ps(r, b));
+                                t = (b - NQ < NQ) ? fma(h, Ps(r, b - NQ), Ps(r, b)) : Ps(r, b);
 #pragma unroll
-                                for (int s = 0; s < NQ; ++s) t = fma(hFqd[s * NQ + b - NQ], Ps(r, NQ + s), t);
+                                for (int s = 0; s < NA; ++s) t = fma(hFqd[s * NA + b - NQ], Ps(r, NQ + s), t);
                             }
                             tcol[r] = t;
                         }
-                        at_mul<NQ, double>(h, hFq, hFqd, tcol, row);
+                        at_mul<NQ, NA, double>(h, hFq, hFqd, tcol, row);
 #pragma unroll
                         for (int a = 0; a <= b; ++a) Pn[a][b] = row[a] + ((a == b) ? Q[a] : 0.0);
                     }
                     double t[NX];
-                    at_mul<NQ, double>(h, hFq, hFqd, mv, t);
+                    at_mul<NQ, NA, double>(h, hFq, hFqd, mv, t);
 #pragma unroll
                     for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - tr[(k - 1) * NX + q], t[q]);
 #pragma unroll
@@ -514,16 +518,14 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             }
             // software pipeline: K_{k+1} (HBM) and the LDS operands of step k+1 are loaded during step k
             constexpr int NK = NU * (NS + 1);
-            double nK[NK], nFq[NQ * NQ], nFqd[NQ * NQ], nFu[NQ * NU], nF[NX], nc[NX], nr[NX], nu_[NU];
+            double nK[NK], nFq[SQ], nFqd[FD], nFu[FU], nF[NX], nc[NX], nr[NX], nu_[NU];
 #define GROUP_LOAD_STEP(k_)                                                                        \
         do {                                                                                           \
             const int kk_ = (k_);                                                                      \
             _Pragma("unroll") for (int i_ = 0; i_ < NK; ++i_) nK[i_] = wK[kk_ * NK + i_];              \
-            _Pragma("unroll") for (int i_ = 0; i_ < NQ * NQ; ++i_) {                                   \
-            nFq[i_] = sFq[kk_ * NQ * NQ + i_];                                                     \
-            nFqd[i_] = sFqd[kk_ * NQ * NQ + i_];                                                   \
-            }                                                                                          \
-            _Pragma("unroll") for (int i_ = 0; i_ < NQ * NU; ++i_) nFu[i_] = sFu[kk_ * NQ * NU + i_];  \
+            _Pragma("unroll") for (int i_ = 0; i_ < FQ; ++i_) nFq[i_] = sFq[kk_ * FQ + i_];             \
+            _Pragma("unroll") for (int i_ = 0; i_ < FD; ++i_) nFqd[i_] = sFqd[kk_ * FD + i_];           \
+            _Pragma("unroll") for (int i_ = 0; i_ < FU; ++i_) nFu[i_] = sFu[kk_ * FU + i_];             \
             _Pragma("unroll") for (int r_ = 0; r_ < NX; ++r_) {                                        \
             nF[r_] = sF[kk_ * NX + r_];                                                            \
             nc[r_] = sC[kk_ * NX + r_];                                                            \
@@ -537,16 +539,15 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             constexpr int kStepUnroll = NX <= 4 ? 2 : 1;
 #pragma unroll kStepUnroll
             for (int k = 0; k < N; ++k) {
-                double K[NK], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU], Fk[NX], ck[NX], rk[NX], uk[NU];
+                double K[NK], hFq[SQ], hFqd[FD], hFu[FU], Fk[NX], ck[NX], rk[NX], uk[NU];
 #pragma unroll
                 for (int i = 0; i < NK; ++i) K[i] = nK[i];
 #pragma unroll
-                for (int i = 0; i < NQ * NQ; ++i) {
-                    hFq[i] = nFq[i];
-                    hFqd[i] = nFqd[i];
-                }
+                for (int i = 0; i < FQ; ++i) hFq[i] = nFq[i];
 #pragma unroll
-                for (int i = 0; i < NQ * NU; ++i) hFu[i] = nFu[i];
+                for (int i = 0; i < FD; ++i) hFqd[i] = nFqd[i];
+#pragma unroll
+                for (int i = 0; i < FU; ++i) hFu[i] = nFu[i];
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
                     Fk[r] = nF[r];
@@ -578,9 +579,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     }
                 }
                 double ad[NX];
-                a_mul<NQ, double>(h, hFq, hFqd, dx, ad);
+                a_mul<NQ, NA, double>(h, hFq, hFqd, dx, ad);
 #pragma unroll
-                for (int s = 0; s < NQ; ++s)
+                for (int s = 0; s < NA; ++s)
 #pragma unroll
                     for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
 #pragma unroll
@@ -609,34 +610,31 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     sD[r] = 0.0;
                 }
                 // the operands of step k+1 are loaded during step k (the recursion is latency-bound)
-                double aq[NQ * NQ], ad[NQ * NQ], ac[NX];
+                double aq[SQ], ad[FD], ac[NX];
 #pragma unroll
-                for (int i = 0; i < NQ * NQ; ++i) {
-                    aq[i] = sFq[i];
-                    ad[i] = sFqd[i];
-                }
+                for (int i = 0; i < FQ; ++i) aq[i] = sFq[i];
+#pragma unroll
+                for (int i = 0; i < FD; ++i) ad[i] = sFqd[i];
 #pragma unroll
                 for (int r = 0; r < NX; ++r) ac[r] = sC[r];
                 constexpr int kDUnroll = NX <= 4 ? 2 : 1;
 #pragma unroll kDUnroll
                 for (int k = 0; k < N; ++k) {
-                    double fq[NQ * NQ], fd[NQ * NQ], cc[NX], dn[NX];
+                    double fq[SQ], fd[FD], cc[NX], dn[NX];
 #pragma unroll
-                    for (int i = 0; i < NQ * NQ; ++i) {
-                        fq[i] = aq[i];
-                        fd[i] = ad[i];
-                    }
+                    for (int i = 0; i < FQ; ++i) fq[i] = aq[i];
+#pragma unroll
+                    for (int i = 0; i < FD; ++i) fd[i] = ad[i];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) cc[r] = ac[r];
                     const int kn = k + 1 < N ? k + 1 : k;
 #pragma unroll
-                    for (int i = 0; i < NQ * NQ; ++i) {
-                        aq[i] = sFq[kn * NQ * NQ + i];
-                        ad[i] = sFqd[kn * NQ * NQ + i];
-                    }
+                    for (int i = 0; i < FQ; ++i) aq[i] = sFq[kn * FQ + i];
+#pragma unroll
+                    for (int i = 0; i < FD; ++i) ad[i] = sFqd[kn * FD + i];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) ac[r] = sC[kn * NX + r];
-                    a_mul<NQ, double>(h, fq, fd, d, dn);
+                    a_mul<NQ, NA, double>(h, fq, fd, d, dn);
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         d[r] = dn[r] + cc[r];

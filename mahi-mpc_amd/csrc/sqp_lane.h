@@ -30,10 +30,23 @@ namespace mmpc {
 // Workspace layout, stage-major: [64-instance block][stage k = 0..N+1][field][lane].  All fields of
 // stage k sit at compile-time offsets from one wave-uniform base, so an access is base(k) + const in
 // scalar registers plus the lane offset in one VGPR (an [element][lane] layout hoists one 64-bit
-// per-lane pointer per (field, element) and spills).  Stage N holds x_N, d_N, dx_N; stage N+1 holds
-// the linear-mode data; stage N+2 is per-lane scratch for the Riccati step (W = P_xx A).
+// per-lane pointer per (field, element) and spills).  Stage N holds x_N, d_N, dx_N; stages N+1.. hold
+// the linear-mode data (one stage for the built-in models); the stage(s) after it are per-lane scratch for
+// the Riccati step (W = P_xx A).  A field block longer than a stage simply runs on into the next stage.
 __host__ __device__ constexpr int lane_stage_stride(int nx, int nu) { return 5 * nx + 3 * nu + nu * (nx + nu + 1); }
-__host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int N) { return (N + 3) * lane_stage_stride(nx, nu); }
+// linear-mode block: h-free Jacobian blocks da/dq (na x nq), da/dz (na x na), da/du (na x nu), xdot*, x*, u*
+__host__ __device__ constexpr int lane_lin_doubles(int nx, int nu, int nq) {
+    return (nx - nq) * (nq + (nx - nq) + nu) + 2 * nx + nu;
+}
+__host__ __device__ constexpr int lane_lin_stages(int nx, int nu, int nq) {
+    return (lane_lin_doubles(nx, nu, nq) + lane_stage_stride(nx, nu) - 1) / lane_stage_stride(nx, nu);
+}
+__host__ __device__ constexpr int lane_scratch_stages(int nx, int nu) {
+    return (nx * nx + lane_stage_stride(nx, nu) - 1) / lane_stage_stride(nx, nu);
+}
+__host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int nq, int N) {
+    return (N + 1 + lane_lin_stages(nx, nu, nq) + lane_scratch_stages(nx, nu)) * lane_stage_stride(nx, nu);
+}
 template <int NX, int NU>
 struct StageFields {
     static constexpr int NS = NX + NU;
@@ -48,7 +61,6 @@ struct StageFields {
     static constexpr int HOLD = K + NU * (NS + 1);  // bounded solves: bound u_k is held at, NaN = free
     static constexpr int SS = HOLD + NU;
     static_assert(SS == lane_stage_stride(NX, NU), "layout");
-    static_assert(NX * NX <= SS, "Riccati scratch W fits one stage");
 };
 
 struct LaneWork {
@@ -60,32 +72,39 @@ __host__ __device__ constexpr int sym_idx(int n, int i, int j) {
     return i <= j ? i * n - i * (i - 1) / 2 + (j - i) : j * n - j * (j - 1) / 2 + (i - j);
 }
 
-// Products with the discrete stage matrices of a second-order model (x = [q; qd], xdot = [qd; acc]):
-//   A = I + h f_x = [[I, h I], [hFq, I + hFqd]],   B = h f_u = [[0], [hFu]]
-// where hFq = h dacc/dq, hFqd = h dacc/dqd, hFu = h dacc/du (row-major NQ x NQ / NQ x NU).
-template <int NQ, class T>
+// Products with the discrete stage matrices of a model with NQ kinematic rows (x = [q; z], qdot_i = z_i for
+// i < NQ, zdot = a(x, u) with NA = NX - NQ >= NQ rows; second-order models have NA = NQ, a general first-order
+// model NQ = 0):
+//   A = I + h f_x = [[I, h [I 0]], [hFq, I + hFqd]],   B = h f_u = [[0], [hFu]]
+// where hFq = h da/dq (NA x NQ), hFqd = h da/dz (NA x NA), hFu = h da/du (NA x NU), all row-major.  For
+// NA = NQ the FMA order is that of the second-order-only version (same instructions, same rounding).
+template <int NQ, int NA, class T>
 MMPC_HD void a_mul(T h, const T* hFq, const T* hFqd, const T* v, T* out) {
+    constexpr int NM = NQ > NA ? NQ : NA;
 #pragma unroll
-    for (int i = 0; i < NQ; ++i) {
+    for (int i = 0; i < NA; ++i) {
         T t = v[NQ + i];
 #pragma unroll
-        for (int s = 0; s < NQ; ++s) t = fma(hFq[i * NQ + s], v[s], fma(hFqd[i * NQ + s], v[NQ + s], t));
+        for (int s = 0; s < NM; ++s) {
+            if (s < NA) t = fma(hFqd[i * NA + s], v[NQ + s], t);
+            if (s < NQ) t = fma(hFq[i * NQ + s], v[s], t);
+        }
         out[NQ + i] = t;
     }
 #pragma unroll
     for (int i = 0; i < NQ; ++i) out[i] = fma(h, v[NQ + i], v[i]);
 }
-template <int NQ, class T>
+template <int NQ, int NA, class T>
 MMPC_HD void at_mul(T h, const T* hFq, const T* hFqd, const T* v, T* out) {
 #pragma unroll
-    for (int a = 0; a < NQ; ++a) {
-        T tq = v[a], td = fma(h, v[a], v[NQ + a]);
+    for (int a = 0; a < NA; ++a) {
+        T tq = a < NQ ? v[a] : T(0), td = a < NQ ? fma(h, v[a], v[NQ + a]) : v[NQ + a];
 #pragma unroll
-        for (int s = 0; s < NQ; ++s) {
-            tq = fma(hFq[s * NQ + a], v[NQ + s], tq);
-            td = fma(hFqd[s * NQ + a], v[NQ + s], td);
+        for (int s = 0; s < NA; ++s) {
+            if (a < NQ) tq = fma(hFq[s * NQ + a], v[NQ + s], tq);
+            td = fma(hFqd[s * NA + a], v[NQ + s], td);
         }
-        out[a] = tq;
+        if (a < NQ) out[a] = tq;
         out[NQ + a] = td;
     }
 }
@@ -104,8 +123,9 @@ __device__ __forceinline__ double* stage_ptr(double* wsb, int64_t k, int SS, int
 // merit and iterates stay fp64, so every SQP iteration refines the fp32 step against fp64 residuals).
 template <class Model, class FT = double, bool BOUNDED = false>
 __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw) {
-    constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NS = NX + NU, ND = NX + NU;
-    static_assert(NX == 2 * NQ, "second-order models only (x = [q; qd])");
+    constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
+    constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)
+    static_assert(NQ >= 0 && NA >= NQ, "x = [q; z] with qdot = z[0:NQ]");
     const int64_t inst = blockIdx.x * (int64_t)64 + threadIdx.x;
     const int lane0 = threadIdx.x;
     MMPC_PHASE_DECL
@@ -121,7 +141,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     using SF = StageFields<NX, NU>;
     constexpr int SS = SF::SS;
     const int lane = threadIdx.x;
-    double* __restrict__ const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)(N + 3) * SS * 64);  // wave-uniform
+    double* __restrict__ const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)lane_ws_doubles(NX, NU, NQ, N) * 64);  // wave-uniform
+    const int kScratch = N + 1 + lane_lin_stages(NX, NU, NQ);  // first stage of the W = P_xx A scratch
 #define ST(k, f, e) wsb[((int64_t)(k) * SS + (f) + (e)) * 64 + lane]  // one-off accesses
 #define SK(dk, f, e) sk[((dk) * SS + (f) + (e)) * 64]                   // stage k + dk inside a stage loop
 
@@ -156,26 +177,24 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     }
     // linear mode: acceleration Jacobians and xdot at (state, control) = (x_0, u_prev), ModelControl.cpp:125-135
     const bool lin = p.is_linear != 0;
-    constexpr int LFQ = 0, LFQD = NQ * NQ, LFU = 2 * NQ * NQ, LXD = 2 * NQ * NQ + NQ * NU, LXS = LXD + NX,
+    constexpr int LFQ = 0, LFQD = NA * NQ, LFU = LFQD + NA * NA, LXD = LFU + NA * NU, LXS = LXD + NX,
                   LUS = LXS + NX;
-    static_assert(LUS + NU <= SS, "linear-mode block fits one stage");
+    static_assert(LUS + NU == lane_lin_doubles(NX, NU, NQ), "linear-mode block layout");
     if (lin) {
-        double x[NX], acc[NQ], Fq[NQ * NQ], Fqd[NQ * NQ], Fu[NQ * NU];
+        double x[NX], acc[NA], Fq[SQ], Fqd[NA * NA], Fu[NA * NU];
 #pragma unroll
         for (int r = 0; r < NX; ++r) x[r] = ST(0, SF::X, r);
         Model::eval_acc_jac(x, up, acc, Fq, Fqd, Fu);
 #pragma unroll
-        for (int t = 0; t < NQ * NQ; ++t) {
-            ST(N + 1, LFQ, t) = Fq[t];
-            ST(N + 1, LFQD, t) = Fqd[t];
-        }
+        for (int t = 0; t < NA * NQ; ++t) ST(N + 1, LFQ, t) = Fq[t];
 #pragma unroll
-        for (int t = 0; t < NQ * NU; ++t) ST(N + 1, LFU, t) = Fu[t];
+        for (int t = 0; t < NA * NA; ++t) ST(N + 1, LFQD, t) = Fqd[t];
 #pragma unroll
-        for (int t = 0; t < NQ; ++t) {
-            ST(N + 1, LXD, t) = x[NQ + t];
-            ST(N + 1, LXD, NQ + t) = acc[t];
-        }
+        for (int t = 0; t < NA * NU; ++t) ST(N + 1, LFU, t) = Fu[t];
+#pragma unroll
+        for (int t = 0; t < NQ; ++t) ST(N + 1, LXD, t) = x[NQ + t];
+#pragma unroll
+        for (int t = 0; t < NA; ++t) ST(N + 1, LXD, NQ + t) = acc[t];
 #pragma unroll
         for (int t = 0; t < NX; ++t) ST(N + 1, LXS, t) = x[t];
 #pragma unroll
@@ -197,16 +216,20 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             double dx_[NX], du_[NU];                                                                     \
             _Pragma("unroll") for (int i_ = 0; i_ < NX; ++i_) dx_[i_] = x[i_] - lp_[((LXS) + (i_)) * 64];        \
             _Pragma("unroll") for (int i_ = 0; i_ < NU; ++i_) du_[i_] = u[i_] - lp_[((LUS) + (i_)) * 64];        \
-            _Pragma("unroll") for (int i_ = 0; i_ < NQ; ++i_) {                                          \
-                xd[i_] = lp_[((LXD) + (i_)) * 64] + dx_[NQ + i_];                                                \
+            _Pragma("unroll") for (int i_ = 0; i_ < NQ; ++i_) xd[i_] = lp_[((LXD) + (i_)) * 64] + dx_[NQ + i_];  \
+            _Pragma("unroll") for (int i_ = 0; i_ < NA; ++i_) {                                          \
                 double t_ = lp_[((LXD) + (NQ + i_)) * 64];                                                       \
-                _Pragma("unroll") for (int s_ = 0; s_ < NQ; ++s_) {                                      \
-                    const double fq_ = lp_[((LFQ) + (i_ * NQ + s_)) * 64], fd_ = lp_[((LFQD) + (i_ * NQ + s_)) * 64];   \
-                    if (jac) {                                                                           \
-                        hFq[i_ * NQ + s_] = fq_;                                                         \
-                        hFqd[i_ * NQ + s_] = fd_;                                                        \
+                _Pragma("unroll") for (int s_ = 0; s_ < (NQ > NA ? NQ : NA); ++s_) {                      \
+                    if (s_ < NA) {                                                                       \
+                        const double fd_ = lp_[((LFQD) + (i_ * NA + s_)) * 64];                          \
+                        if (jac) hFqd[i_ * NA + s_] = fd_;                                               \
+                        t_ = fma(fd_, dx_[NQ + s_], t_);                                                 \
                     }                                                                                    \
-                    t_ = fma(fq_, dx_[s_], fma(fd_, dx_[NQ + s_], t_));                                  \
+                    if (s_ < NQ) {                                                                       \
+                        const double fq_ = lp_[((LFQ) + (i_ * NQ + s_)) * 64];                           \
+                        if (jac) hFq[i_ * NQ + s_] = fq_;                                                \
+                        t_ = fma(fq_, dx_[s_], t_);                                                      \
+                    }                                                                                    \
                 }                                                                                        \
                 _Pragma("unroll") for (int c_ = 0; c_ < NU; ++c_) {                                      \
                     const double fu_ = lp_[((LFU) + (i_ * NU + c_)) * 64];                                       \
@@ -217,11 +240,9 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             }                                                                                            \
         }                                                                                                \
         if (jac) {                                                                                       \
-            _Pragma("unroll") for (int i_ = 0; i_ < NQ * NQ; ++i_) {                                     \
-                hFq[i_] *= h;                                                                            \
-                hFqd[i_] *= h;                                                                           \
-            }                                                                                            \
-            _Pragma("unroll") for (int i_ = 0; i_ < NQ * NU; ++i_) hFu[i_] *= h;                         \
+            _Pragma("unroll") for (int i_ = 0; i_ < NA * NQ; ++i_) hFq[i_] *= h;                         \
+            _Pragma("unroll") for (int i_ = 0; i_ < NA * NA; ++i_) hFqd[i_] *= h;                        \
+            _Pragma("unroll") for (int i_ = 0; i_ < NA * NU; ++i_) hFu[i_] *= h;                         \
         }                                                                                                \
     } while (0)
 
@@ -252,7 +273,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             #pragma unroll 1
             for (int k = 0; k < N; ++k) {
                 double* const sk = stage_ptr(wsb, k, SS, lane);
-                double u[NU], xn[NX], rk[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+                double u[NU], xn[NX], rk[NX], xd[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU];
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
                     u[c] = un[c];
@@ -265,7 +286,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 }
                 STAGE_EVAL(xk, u, xd, hFq, hFqd, hFu, true);
                 double dn[NX];
-                a_mul<NQ>(h, hFq, hFqd, d, dn);
+                a_mul<NQ, NA>(h, hFq, hFqd, d, dn);
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
                     const double F = fma(h, xd[r], xk[r]);
@@ -333,8 +354,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 #pragma unroll 1
                 for (int k = N - 1; k >= 0; --k) {
                     double* const sk = stage_ptr(wsb, k, SS, lane);
-                    double x[NX], u[NU], um[NU], cc[NX], dk[NX], rkm[NX], xd[NX], hFq[NQ * NQ], hFqd[NQ * NQ],
-                        hFu[NQ * NU], tg[NU];
+                    double x[NX], u[NU], um[NU], cc[NX], dk[NX], rkm[NX], xd[NX], hFq[SQ], hFqd[NA * NA],
+                        hFu[NA * NU], tg[NU];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         x[r] = xpf[r];
@@ -365,7 +386,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     for (int c = 0; c < NU; ++c) {
                         double g = 0.0;
 #pragma unroll
-                        for (int s = 0; s < NQ; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
+                        for (int s = 0; s < NA; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
                         g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
                         if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
                         if (!BOUNDED) {
@@ -387,7 +408,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1},  e_{k-1} = d_k + x_k - r_{k-1}
                     if (k >= 1) {
                         double ln[NX];
-                        at_mul<NQ>(h, hFq, hFqd, lam, ln);
+                        at_mul<NQ, NA>(h, hFq, hFqd, lam, ln);
 #pragma unroll
                         for (int r = 0; r < NX; ++r) {
                             lam[r] = fma(Q[r], dk[r] + x[r] - rkm[r], ln[r]);
@@ -399,15 +420,14 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     // right-hand side (p, m = P_xx c + p_x, h_w, y, kff) in fp64 with FT matrices: with FT = float
                     // this is an fp32 factorisation applied to fp64 residuals, so each SQP iteration is a
                     // refinement step (the linear terms cancel down to the gradient and need fp64).
-                    FT fq[NQ * NQ], fqd[NQ * NQ], fu[NQ * NU];
+                    FT fq[SQ], fqd[NA * NA], fu[NA * NU];
                     const FT hf = (FT)h;
 #pragma unroll
-                    for (int i = 0; i < NQ * NQ; ++i) {
-                        fq[i] = (FT)hFq[i];
-                        fqd[i] = (FT)hFqd[i];
-                    }
+                    for (int i = 0; i < NA * NQ; ++i) fq[i] = (FT)hFq[i];
 #pragma unroll
-                    for (int i = 0; i < NQ * NU; ++i) fu[i] = (FT)hFu[i];
+                    for (int i = 0; i < NA * NA; ++i) fqd[i] = (FT)hFqd[i];
+#pragma unroll
+                    for (int i = 0; i < NA * NU; ++i) fu[i] = (FT)hFu[i];
                     FT G[NX][NU];  // P_xx B + P_xu   (B = [0; hFu])
 #pragma unroll
                     for (int r = 0; r < NX; ++r)
@@ -415,7 +435,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         for (int c = 0; c < NU; ++c) {
                             FT t = PS(r, NX + c);
 #pragma unroll
-                            for (int s = 0; s < NQ; ++s) t = fma(PS(r, NQ + s), fu[s * NU + c], t);
+                            for (int s = 0; s < NA; ++s) t = fma(PS(r, NQ + s), fu[s * NU + c], t);
                             G[r][c] = t;
                         }
                     double mv[NX];  // P_xx c + p_x (fp64)
@@ -434,21 +454,21 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         for (int b = a; b < NU; ++b) {
                             FT t = PS(NX + a, NX + b);
 #pragma unroll
-                            for (int s = 0; s < NQ; ++s)
+                            for (int s = 0; s < NA; ++s)
                                 t = fma(fu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), fu[s * NU + b], t));
                             if (a == b) t += (FT)(R[a] + Rm[a]);
                             Hww[a][b] = t;
                         }
                         double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
 #pragma unroll
-                        for (int s = 0; s < NQ; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
+                        for (int s = 0; s < NA; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
 #pragma unroll
                         for (int r = 0; r < NX; ++r) t = fma((double)PS(r, NX + a), cc[r], t);
                         yh[a] = t;
                         FT ga[NX];
 #pragma unroll
                         for (int r = 0; r < NX; ++r) ga[r] = G[r][a];
-                        at_mul<NQ, FT>(hf, fq, fqd, ga, &Y[a][0]);  // H_wx row a = (A^T G[:, a])^T
+                        at_mul<NQ, NA, FT>(hf, fq, fqd, ga, &Y[a][0]);  // H_wx row a = (A^T G[:, a])^T
 #pragma unroll
                         for (int c = 0; c < NU; ++c) Y[a][NX + c] = (FT)((a == c) ? -R[a] : 0.0);
                     }
@@ -494,19 +514,19 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     // workspace (in registers next to G, Y and the stage blocks it spills).
                     // p~_k x part: A^T mv + Q (x_k - r_{k-1}) (fp64).
                     double pn[NS];
-                    FT* const sw = reinterpret_cast<FT*>(stage_ptr(wsb, N + 2, SS, 0)) + lane;  // per-lane scratch stage
+                    FT* const sw = reinterpret_cast<FT*>(stage_ptr(wsb, kScratch, SS, 0)) + lane;  // per-lane scratch stage
                     if (k >= 1) {
 #pragma unroll
                         for (int r = 0; r < NX; ++r) {
                             FT prow[NX], wrow[NX];
 #pragma unroll
                             for (int q = 0; q < NX; ++q) prow[q] = PS(r, q);
-                            at_mul<NQ, FT>(hf, fq, fqd, prow, wrow);
+                            at_mul<NQ, NA, FT>(hf, fq, fqd, prow, wrow);
 #pragma unroll
                             for (int b = 0; b < NX; ++b) sw[(r * NX + b) * 64] = wrow[b];
                         }
                         double t[NX];
-                        at_mul<NQ, double>(h, hFq, hFqd, mv, t);
+                        at_mul<NQ, NA, double>(h, hFq, hFqd, mv, t);
 #pragma unroll
                         for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - rkm[q], t[q]);
 #pragma unroll
@@ -580,7 +600,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         FT wcol[NX], col[NX];
 #pragma unroll
                         for (int r = 0; r < NX; ++r) wcol[r] = sw[(r * NX + b) * 64];
-                        at_mul<NQ, FT>(hf, fq, fqd, wcol, col);
+                        at_mul<NQ, NA, FT>(hf, fq, fqd, wcol, col);
 #pragma unroll
                         for (int a = 0; a <= b; ++a) {
                             FT v = col[a] + (FT)((a == b) ? Q[a] : 0.0);
@@ -663,7 +683,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 #pragma unroll 1
                 for (int k = 0; k < N; ++k) {
                     double* const sk = stage_ptr(wsb, k, SS, lane);
-                    double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[NQ * NQ], hFqd[NQ * NQ], hFu[NQ * NU];
+                    double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         x[r] = xpf[r];
@@ -702,9 +722,9 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     }
                     STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
                     double ad[NX];
-                    a_mul<NQ>(h, hFq, hFqd, dx, ad);
+                    a_mul<NQ, NA>(h, hFq, hFqd, dx, ad);
 #pragma unroll
-                    for (int s = 0; s < NQ; ++s)
+                    for (int s = 0; s < NA; ++s)
 #pragma unroll
                         for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
 #pragma unroll

@@ -20,19 +20,31 @@ int main(int argc, char** argv) {
     const int N = argc > 1 ? std::atoi(argv[1]) : 20;
     const double sim_seconds = argc > 2 ? std::atof(argv[2]) : 0.2;
     const bool linear = argc > 3 && argv[3][0] == 'l';
-    const std::string name = linear ? "linear_double_pendulum" : "nonlinear_double_pendulum";
-    ModelParameters mp(name, 4, 2, mahi::util::milliseconds(2), N, linear);
-    ModelGenerator gen(mp, "two_link_arm");
-    gen.create_model();
-    gen.generate_c_code();
-    gen.compile_model();
+    // optional 4th argument: the path (without .json) of a model generated beforehand from SX expressions
+    // (ex_model_generate): ModelControl then loads its own solver library through the JSON's dll_filepath
+    const std::string model_path = argc > 4 ? argv[4] : "";
+    std::string name = linear ? "linear_double_pendulum" : "nonlinear_double_pendulum";
+    if (model_path.empty()) {
+        ModelParameters mp(name, 4, 2, mahi::util::milliseconds(2), N, linear);
+        ModelGenerator gen(mp, "two_link_arm");
+        gen.create_model();
+        gen.generate_c_code();
+        gen.compile_model();
+    } else {
+        name = model_path;
+    }
 
     ModelControl mc(name, {10, 1, 5, 5}, {5, 5}, {0.01, 0.01});
+    if (mc.model_parameters.num_shooting_nodes != N) {
+        std::fprintf(stderr, "model %s has N = %d\n", name.c_str(), mc.model_parameters.num_shooting_nodes);
+        return 2;
+    }
+    const std::string ext_name = mc.model_parameters.name;
     const int nx = mc.model_parameters.num_x;
     const double h = mc.model_parameters.step_size.as_seconds();
     std::vector<double> state(4, 0.0), control(2, 0.0);
     // plant model through the generated CasADi external, as model_control_example.cpp:46
-    auto ext_x_dot_init = external(name + "_get_x_dot_init", name + "_linear_functions.so");
+    auto ext_x_dot_init = external(ext_name + "_get_x_dot_init", name + "_linear_functions.so");
     const double PI = 3.14159265358979323846, sin_amp = 1.0, sin_freq = 1.0;
     double t = 0.0;
     int cycle = 0;

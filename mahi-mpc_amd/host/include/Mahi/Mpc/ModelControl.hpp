@@ -4,6 +4,7 @@
 #pragma once
 #include <atomic>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -65,6 +66,8 @@ public:
                                                   std::vector<int>* status = nullptr);
 
 private:
+    struct Backend;                     // the C-ABI entry points of the model's library (dll_filepath)
+    std::shared_ptr<Backend> m_backend;
     Dict m_solver_opts;
     mahi::util::Time curr_time;
     mmpc_handle* m_handle = nullptr;

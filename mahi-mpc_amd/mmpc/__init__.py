@@ -40,7 +40,9 @@ class MmpcError(RuntimeError):
 
 
 KKT_AUTO, KKT_CONDENSED, KKT_RICCATI, KKT_RICCATI_GROUP = 0, 1, 2, 3
-MODEL_TWO_LINK_ARM, MODEL_EXO_ARM = 0, 1
+MODEL_TWO_LINK_ARM, MODEL_EXO_ARM, MODEL_USER = 0, 1, 2
+USER_LIB_DIR = os.path.join(ROOT, "lib", "user")
+BUILTIN_MODELS = ("two_link_arm", "double_pendulum", "exo_arm", "exo")  # "mmpc_model" names libmmpc.so serves   # models generated from SX by ModelGenerator (make -C host user)
 
 
 class Opts(C.Structure):
@@ -56,7 +58,7 @@ class ModelInfo(C.Structure):
                 ("x_min", C.c_double * 16), ("x_max", C.c_double * 16)]
 
 
-_lib = None
+_libs = {}
 _vp = C.c_void_p
 
 
@@ -75,11 +77,12 @@ def header_functions(path: str = HEADER_PATH):
     return sorted(set(re.findall(r"\b(mmpc_\w+)\s*\(", text)))
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise MmpcError(-2, f"{LIB_PATH} not built (run make -C mahi-mpc_amd)")
+def lib(path: str | None = None):
+    """The C-ABI library: libmmpc.so (built-in models) or a model's generated <name>.so (same ABI)."""
+    path = os.path.abspath(path or LIB_PATH)
+    if path not in _libs:
+        if not os.path.exists(path):
+            raise MmpcError(-2, f"{path} not built (run make -C mahi-mpc_amd)")
         # PyTorch-ROCm ships its own HIP runtime: if libmmpc's initialises first, torch later sees no GPU
         # (observed on the MI355X box), so torch -- when present -- initialises before the library is loaded
         try:
@@ -87,7 +90,7 @@ def lib():
             torch.cuda.is_available()
         except ImportError:
             pass
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)  # RTLD_LOCAL: each model library keeps its own kernels (linked with -Bsymbolic)
         L.mmpc_abi_version.restype = C.c_int
         L.mmpc_default_opts.argtypes = [C.POINTER(Opts)]
         L.mmpc_create.argtypes = [C.c_char_p, C.POINTER(Opts), C.POINTER(_vp)]
@@ -106,13 +109,33 @@ def lib():
         L.mmpc_status_string.argtypes = [C.c_int32]
         L.mmpc_status_string.restype = C.c_char_p
         L.mmpc_last_error.restype = C.c_char_p
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
-def _check(rc):
+def model_library(model_json: str) -> str:
+    """Library serving the model of <name>.json: for a model generated from SX expressions ("mmpc_model" naming
+    no built-in model) its dll_filepath, resolved against the JSON's directory as ModelControl does; else
+    libmmpc.so (built-in models, and reference-written JSONs whose dll_filepath is a CasADi NLP library)."""
+    try:
+        with open(model_json) as fh:
+            m = json.load(fh)
+    except (OSError, ValueError):
+        return LIB_PATH  # mmpc_create reports the I/O or parse error
+    m = m.get("model", m) if isinstance(m, dict) else {}
+    dll = m.get("dll_filepath") or ""
+    if m.get("mmpc_model") in (None, *BUILTIN_MODELS) or not dll or os.path.basename(dll) == "libmmpc.so":
+        return LIB_PATH
+    cands = [dll] if os.path.isabs(dll) else [os.path.join(os.path.dirname(os.path.abspath(model_json)), dll), dll]
+    for c in cands:
+        if os.path.exists(c):
+            return os.path.abspath(c)
+    raise MmpcError(-2, f"model library {dll} of {model_json} not found")
+
+
+def _check(rc, L=None):
     if rc != OK:
-        raise MmpcError(rc, lib().mmpc_last_error().decode())
+        raise MmpcError(rc, (L or lib()).mmpc_last_error().decode())
 
 
 def default_opts() -> Opts:
@@ -167,8 +190,10 @@ class Solver:
     """One loaded model (the reference's ModelControl without the thread/bookkeeping)."""
 
     def __init__(self, model_json=None, json_text=None, max_iter=None, tol_grad=None, tol_defect=None,
-                 device=None, kkt_solver=None, factor_fp32=None):
-        o = default_opts()
+                 device=None, kkt_solver=None, factor_fp32=None, library=None):
+        self._L = L = lib(library or (model_library(model_json) if model_json is not None else None))
+        o = Opts()
+        L.mmpc_default_opts(C.byref(o))
         if kkt_solver is not None:
             o.kkt_solver = kkt_solver
         if factor_fp32 is not None:
@@ -183,26 +208,29 @@ class Solver:
             o.device = device
         h = _vp()
         if json_text is not None:
-            _check(lib().mmpc_create_from_json(json_text.encode(), C.byref(o), C.byref(h)))
+            self._check(L.mmpc_create_from_json(json_text.encode(), C.byref(o), C.byref(h)))
         else:
-            _check(lib().mmpc_create(os.fsencode(model_json), C.byref(o), C.byref(h)))
+            self._check(L.mmpc_create(os.fsencode(model_json), C.byref(o), C.byref(h)))
         self._h = h
         info = ModelInfo()
-        _check(lib().mmpc_get_model_info(h, C.byref(info)))
+        self._check(L.mmpc_get_model_info(h, C.byref(info)))
         self.info = info
         self.nx, self.nu, self.N = info.num_x, info.num_u, info.num_shooting_nodes
         self.NV = info.num_v
         self.h = info.step_size
 
+    def _check(self, rc):
+        _check(rc, self._L)
+
     def reserve_workspace(self, B) -> int:
         """Pre-allocate the Riccati solver workspace for up to B instances; returns its size in bytes."""
         n = C.c_uint64(0)
-        _check(lib().mmpc_reserve_workspace(self._h, B, C.byref(n)))
+        self._check(self._L.mmpc_reserve_workspace(self._h, B, C.byref(n)))
         return int(n.value)
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().mmpc_destroy(self._h)
+            self._L.mmpc_destroy(self._h)
             self._h = None
 
     def __del__(self):
@@ -214,19 +242,19 @@ class Solver:
     # ---- device-pointer API (torch tensors on the GPU or raw addresses) ----
     def solve_batch(self, B, x0, u_prev, traj, weights, V, status=None, iters=None, kkt=None,
                     weights_stride=0, u_lb=None, u_ub=None, stream=None):
-        _check(lib().mmpc_solve_batch(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights),
+        self._check(self._L.mmpc_solve_batch(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights),
                                       weights_stride, _ptr(u_lb), _ptr(u_ub), _ptr(V), _ptr(status),
                                       _ptr(iters), _ptr(kkt), stream))
 
     def synth(self, seed, first_index, B, x0, u_prev, traj, stream=None):
-        _check(lib().mmpc_synth_batch(self._h, seed, first_index, B, _ptr(x0), _ptr(u_prev), _ptr(traj), stream))
+        self._check(self._L.mmpc_synth_batch(self._h, seed, first_index, B, _ptr(x0), _ptr(u_prev), _ptr(traj), stream))
 
     def nlp_eval(self, B, V, u_prev, traj, weights, J, defect_inf, weights_stride=0, stream=None):
-        _check(lib().mmpc_nlp_eval_batch(self._h, B, _ptr(V), _ptr(u_prev), _ptr(traj), _ptr(weights),
+        self._check(self._L.mmpc_nlp_eval_batch(self._h, B, _ptr(V), _ptr(u_prev), _ptr(traj), _ptr(weights),
                                          weights_stride, _ptr(J), _ptr(defect_inf), stream))
 
     def linearize(self, B, x, u, A, Bm, xdot, stream=None):
-        _check(lib().mmpc_linearize_batch(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xdot), stream))
+        self._check(self._L.mmpc_linearize_batch(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xdot), stream))
 
     # ---- host (numpy) API, synchronous ----
     def solve_batch_host(self, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None):
@@ -243,14 +271,14 @@ class Solver:
         kkt = np.zeros(B)
         lb = None if u_lb is None else _f64(u_lb)
         ub = None if u_ub is None else _f64(u_ub)
-        _check(lib().mmpc_solve_batch_host(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights), ws,
+        self._check(self._L.mmpc_solve_batch_host(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights), ws,
                                            _ptr(lb), _ptr(ub), _ptr(V), _ptr(st), _ptr(it), _ptr(kkt)))
         return dict(V=V, status=st, iters=it, kkt=kkt)
 
     def kkt_solver_for(self, B: int) -> int:
         """KKT_* solver a solve of B instances runs (the AUTO choice resolved)."""
         v = C.c_int32()
-        _check(lib().mmpc_resolve_kkt_solver(self._h, B, C.byref(v)))
+        self._check(self._L.mmpc_resolve_kkt_solver(self._h, B, C.byref(v)))
         return v.value
 
     def linearize_host(self, x, u):
@@ -259,7 +287,7 @@ class Solver:
         B = x.shape[0]
         u = _f64(u, (B, nu))
         A = np.zeros((B, nx * nx)); Bm = np.zeros((B, nx * nu)); xd = np.zeros((B, nx))
-        _check(lib().mmpc_linearize_batch_host(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xd)))
+        self._check(self._L.mmpc_linearize_batch_host(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xd)))
         # column-major per instance (CasADi DM order) -> (B, nx, nx) row-major views
         return (A.reshape(B, nx, nx).transpose(0, 2, 1), Bm.reshape(B, nu, nx).transpose(0, 2, 1), xd)
 

@@ -34,10 +34,21 @@ static _Thread_local int t_model = ORACLE_MODEL_TWO_LINK_ARM, t_nx = 4, t_nu = 2
 #define NX t_nx
 #define NU t_nu
 #define ND (t_nx + t_nu)
+/* dynamics registered by oracle_set_user_model (process-wide; models generated from SX expressions) */
+static oracle_user_jac_fn g_user_jac = NULL;
+static int g_user_nx = 0, g_user_nu = 0;
 static int set_model(int model) {
     if (model == ORACLE_MODEL_TWO_LINK_ARM) { t_model = model; t_nx = 4; t_nu = 2; return 0; }
     if (model == ORACLE_MODEL_EXO_ARM) { t_model = model; t_nx = 8; t_nu = 4; return 0; }
+    if (model == ORACLE_MODEL_USER && g_user_jac) { t_model = model; t_nx = g_user_nx; t_nu = g_user_nu; return 0; }
     return -1;
+}
+int oracle_set_user_model(int nx, int nu, oracle_user_jac_fn jac) {
+    if (nx < 1 || nx > ORACLE_MAX_NX || nu < 1 || nu > ORACLE_MAX_NU || !jac) return -1;
+    g_user_nx = nx;
+    g_user_nu = nu;
+    g_user_jac = jac;
+    return 0;
 }
 
 /* ---------------- forward-mode dual numbers (6 tangents: x then u of the 2-link arm) ---------------- */
@@ -174,7 +185,10 @@ void oracle_exo_mass(const double* q, double* M) {
 
 static void model_jac(const double* x, const double* u, double* A, double* B, double* xdot) {
     if (t_model == ORACLE_MODEL_EXO_ARM) oracle_exo_jac(x, u, A, B, xdot);
-    else oracle_two_link_jac(x, u, A, B, xdot);
+    else if (t_model == ORACLE_MODEL_USER) {
+        double Af[ORACLE_MAX_NX * ORACLE_MAX_NX], Bf[ORACLE_MAX_NX * ORACLE_MAX_NU];
+        g_user_jac(x, u, A ? A : Af, B ? B : Bf, xdot);
+    } else oracle_two_link_jac(x, u, A, B, xdot);
 }
 
 void oracle_two_link_xdot(const double* x, const double* u, double* xdot) {
@@ -213,7 +227,7 @@ static void stage_jac(const double* x, const double* u, double* A, double* Bc, d
 }
 
 static void euler_step(double h, const double* x, const double* u, double* F, double* Ad, double* Bd) {
-    double A[64], Bc[32], xd[8];
+    double A[ORACLE_MAX_NX * ORACLE_MAX_NX], Bc[ORACLE_MAX_NX * ORACLE_MAX_NU], xd[ORACLE_MAX_NX];
     stage_jac(x, u, A, Bc, xd);
     for (int r = 0; r < NX; ++r) {
         F[r] = x[r] + h * xd[r];
@@ -234,7 +248,7 @@ void oracle_nlp_eval(int model, int N, double h, const double* V, const double* 
         const double* uk = xk + NX;
         const double* xk1 = V + (k + 1) * ND;
         const double* ukm = (k == 0) ? u_prev : V + (k - 1) * ND + NX;
-        double F[8];
+        double F[ORACLE_MAX_NX];
         euler_step(h, xk, uk, F, NULL, NULL);
         for (int r = 0; r < NX; ++r) {
             if (g) g[k * NX + r] = F[r] - xk1[r];
@@ -260,7 +274,7 @@ void oracle_reduced_gradient(int model, int N, double h, const double* x0, const
     memcpy(X, x0, sizeof(double) * NX);
     for (int k = 0; k < N; ++k) euler_step(h, X + k * NX, U + k * NU, X + (k + 1) * NX, Ad + k * NX * NX, Bd + k * NX * NU);
     /* adjoint: lam_{k} = 2Q(x_{k} - r_{k-1}) + A_k^T lam_{k+1}, lam_N = 2Q(x_N - r_{N-1}) */
-    double lam[8], tmp[8];
+    double lam[ORACLE_MAX_NX], tmp[ORACLE_MAX_NX];
     for (int r = 0; r < NX; ++r) lam[r] = 2.0 * Q[r] * (X[N * NX + r] - traj[(N - 1) * NX + r]);
     for (int k = N - 1; k >= 0; --k) {
         /* grad wrt u_k: B_k^T lam_{k+1} */
@@ -386,7 +400,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
      * Gauss-Newton SQP -- the iterate starts projected, controls at a bound whose gradient points outward
      * (epsilon-active set, Bertsekas 1982) are held in the QP, trial points are projected onto the box and the
      * stop test uses the projected gradient ||U - P(U - 2g)||_inf. */
-    double lbv[4], ubv[4];
+    double lbv[ORACLE_MAX_NU], ubv[ORACLE_MAX_NU];
     int has_b = 0;
     for (int q = 0; q < NU; ++q) {
         lbv[q] = (u_lb && u_lb[q] > -1e19) ? u_lb[q] : -INFINITY;
@@ -421,7 +435,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         /* (3) dense Gamma: rows = x_{k+1} (k<N), cols = u_j (j<=k) */
         memset(s->G, 0, sizeof(double) * (size_t)N * NX * M);
         for (int j = 0; j < N; ++j) {
-            double col[8][4], nxt[8][4];
+            double col[ORACLE_MAX_NX][ORACLE_MAX_NU], nxt[ORACLE_MAX_NX][ORACLE_MAX_NU];
             for (int r = 0; r < NX; ++r) for (int q = 0; q < NU; ++q) col[r][q] = s->Bd[j * NX * NU + r * NU + q];
             for (int k = j; k < N; ++k) {
                 if (k > j) {
@@ -544,7 +558,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         if (mu_new > mu) mu = mu_new;
         double J0 = 0.0, c1 = 0.0, dJ = 0.0;
         for (int k = 0; k < N; ++k) {
-            double qe[8];
+            double qe[ORACLE_MAX_NX];
             for (int r = 0; r < NX; ++r) {
                 qe[r] = 2.0 * Q[r] * (s->F[k * NX + r] - traj[k * NX + r]);
                 J0 += 0.5 * qe[r] * (s->F[k * NX + r] - traj[k * NX + r]);
@@ -623,7 +637,7 @@ int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, con
         for (int64_t b = 0; b < B; ++b) {
             int32_t it;
             double kk, J;
-            double lin[64 + 32 + 3 * 8];
+            double lin[ORACLE_MAX_NX * ORACLE_MAX_NX + ORACLE_MAX_NX * ORACLE_MAX_NU + 2 * ORACLE_MAX_NX + ORACLE_MAX_NU];
             if (is_linear) {
                 /* A*, B*, xdot* at (state, control) = (x0, u_prev), ModelControl.cpp:125-136 */
                 model_jac(x0 + b * NX, u_prev + b * NU, lin, lin + NX * NX, lin + NX * NX + NX * NU);

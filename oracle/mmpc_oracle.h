@@ -22,7 +22,16 @@
 extern "C" {
 #endif
 
-enum { ORACLE_MODEL_TWO_LINK_ARM = 0, ORACLE_MODEL_EXO_ARM = 1 };
+enum { ORACLE_MODEL_TWO_LINK_ARM = 0, ORACLE_MODEL_EXO_ARM = 1, ORACLE_MODEL_USER = 2 };
+#define ORACLE_MAX_NX 16
+#define ORACLE_MAX_NU 16
+
+/* Dynamics of a model generated from SX expressions (mahi::mpc::ModelGenerator): continuous Jacobians
+ * A = df/dx (nx x nx), B = df/du (nx x nu) ROW-major and xdot.  The tests register the host build of the
+ * generated <name>_model.h (oracle/user_model_host.cpp), whose expressions are pinned against an independent
+ * sympy restatement of the same model (tests/test_sx_models.py). */
+typedef void (*oracle_user_jac_fn)(const double* x, const double* u, double* A, double* B, double* xdot);
+int oracle_set_user_model(int nx, int nu, oracle_user_jac_fn jac);
 
 /* per-instance status, same numbering as include/mmpc.h */
 enum {

@@ -16,9 +16,11 @@ ORACLE_DIR = os.path.join(ROOT, "oracle")
 LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
 
 NX, NU = 4, 2                       # 2-link arm (model 0)
-TWO_LINK, EXO = 0, 1
+TWO_LINK, EXO, USER = 0, 1, 2
 DIMS = {TWO_LINK: (4, 2), EXO: (8, 4)}
+USER_DIR = os.path.join(ORACLE_DIR, "_user")
 _lib = None
+_user = {}  # host-build path -> (CDLL, dims)
 
 _dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
 _ip = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
@@ -50,6 +52,54 @@ def lib():
         L.oracle_exo_mass.argtypes = [_dp, _dp]
         _lib = L
     return _lib
+
+
+class UserModelHost:
+    """Host build of an SX-generated device model (oracle/_user/<name>_host.so, from <name>_model.h)."""
+
+    def __init__(self, name):
+        path = os.path.join(USER_DIR, f"{name}_host.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} (run make -C mahi-mpc_amd/host user && make -C oracle user)")
+        L = C.CDLL(path)
+        dims = (C.c_int * 3)()
+        L.user_model_dims(C.byref(dims, 0), C.byref(dims, 4), C.byref(dims, 8))
+        self.nx, self.nu, self.nq = dims[0], dims[1], dims[2]
+        self.na = self.nx - self.nq
+        for f, n in (("user_model_eval", 3), ("user_model_eval_acc_jac", 6), ("user_model_jac", 5)):
+            getattr(L, f).restype = None
+            getattr(L, f).argtypes = [C.c_void_p] * n
+        self.L, self.name = L, name
+
+    def eval(self, x, u):
+        xd = np.zeros(self.nx)
+        self.L.user_model_eval(c64(x).ctypes.data, c64(u).ctypes.data, xd.ctypes.data)
+        return xd
+
+    def jac(self, x, u):
+        A = np.zeros(self.nx * self.nx); B = np.zeros(self.nx * self.nu); xd = np.zeros(self.nx)
+        x, u = c64(x), c64(u)
+        self.L.user_model_jac(x.ctypes.data, u.ctypes.data, A.ctypes.data, B.ctypes.data, xd.ctypes.data)
+        return A.reshape(self.nx, self.nx), B.reshape(self.nx, self.nu), xd
+
+    def acc_jac(self, x, u):
+        na, nq, nu = self.na, self.nq, self.nu
+        acc = np.zeros(na); Fq = np.zeros(max(1, na * nq)); Fqd = np.zeros(na * na); Fu = np.zeros(na * nu)
+        x, u = c64(x), c64(u)
+        self.L.user_model_eval_acc_jac(x.ctypes.data, u.ctypes.data, acc.ctypes.data, Fq.ctypes.data,
+                                       Fqd.ctypes.data, Fu.ctypes.data)
+        return acc, Fq[:na * nq].reshape(na, nq), Fqd.reshape(na, na), Fu.reshape(na, nu)
+
+
+def use_user_model(name) -> int:
+    """Register the host build of generated model `name` as the oracle's USER model; returns USER."""
+    m = UserModelHost(name)
+    fn = C.cast(m.L.user_model_jac, C.c_void_p).value
+    lib().oracle_set_user_model.argtypes = [C.c_int, C.c_int, C.c_void_p]
+    assert lib().oracle_set_user_model(m.nx, m.nu, fn) == 0
+    _user["active"] = m  # keep the library loaded
+    DIMS[USER] = (m.nx, m.nu)
+    return USER
 
 
 def c64(a):
