@@ -17,6 +17,9 @@ struct mmpc_handle;
 
 namespace mahi {
 namespace mpc {
+namespace detail {
+struct ModelLibrary;
+}
 
 using Dict = std::map<std::string, double>;
 
@@ -66,8 +69,7 @@ public:
                                                   std::vector<int>* status = nullptr);
 
 private:
-    struct Backend;                     // the C-ABI entry points of the model's library (dll_filepath)
-    std::shared_ptr<Backend> m_backend;
+    std::shared_ptr<detail::ModelLibrary> m_backend;  // C-ABI of the model's library (dll_filepath)
     Dict m_solver_opts;
     mahi::util::Time curr_time;
     mmpc_handle* m_handle = nullptr;

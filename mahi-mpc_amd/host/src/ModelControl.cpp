@@ -12,65 +12,12 @@
 #include <stdexcept>
 
 #include "../../../include/mmpc.h"
+#include "model_library.hpp"
 
 namespace mahi {
 namespace mpc {
 
-// The solver entry points of the model's library.  The reference loads the model's compiled NLP from the JSON's
-// dll_filepath (ModelControl.cpp:62, nlpsol over <name>.so); here a model generated from SX dynamics has its own
-// <name>.so exporting the C-ABI of include/mmpc.h (ModelGenerator::compile_model), and the built-in models are
-// served by the linked libmmpc.so.
-struct ModelControl::Backend {
-    decltype(&mmpc_create_from_json) create_from_json = &mmpc_create_from_json;
-    decltype(&mmpc_destroy) destroy = &mmpc_destroy;
-    decltype(&mmpc_get_model_info) get_model_info = &mmpc_get_model_info;
-    decltype(&mmpc_solve_batch_host) solve_batch_host = &mmpc_solve_batch_host;
-    decltype(&mmpc_last_error) last_error = &mmpc_last_error;
-    void* dl = nullptr;  // kept loaded for the process lifetime (HIP code objects), as CasADi keeps its libraries
-
-    void check(int rc, const char* what) const {
-        if (rc != MMPC_OK) throw std::runtime_error(std::string(what) + ": " + last_error());
-    }
-    template <class F>
-    void bind(F& f, const char* name) {
-        void* s = dlsym(dl, name);
-        if (!s) throw std::runtime_error(std::string("model library lacks ") + name);
-        f = reinterpret_cast<F>(s);
-    }
-    // dll_filepath relative to the JSON's directory first, then to the working directory
-    // A generated model names itself in "mmpc_model"; built-in models (and reference-written JSONs, whose
-    // dll_filepath is a CasADi NLP library) are served by libmmpc.so.
-    static std::shared_ptr<Backend> load(const ModelParameters& mp, const std::string& json_path) {
-        auto b = std::make_shared<Backend>();
-        const std::string& dll = mp.dll_filepath;
-        const size_t sl = dll.rfind('/');
-        const std::string base = sl == std::string::npos ? dll : dll.substr(sl + 1);
-        const std::string& mm = mp.mmpc_model;
-        if (mm.empty() || mm == "two_link_arm" || mm == "double_pendulum" || mm == "exo_arm" || mm == "exo" ||
-            dll.empty() || base == "libmmpc.so")
-            return b;
-        std::vector<std::string> cands;
-        if (dll[0] != '/') {
-            const size_t js = json_path.rfind('/');
-            if (js != std::string::npos) cands.push_back(json_path.substr(0, js + 1) + dll);
-        }
-        cands.push_back(dll[0] == '/' || dll.find('/') != std::string::npos ? dll : "./" + dll);
-        std::string errs;
-        for (const std::string& c : cands) {
-            b->dl = dlopen(c.c_str(), RTLD_NOW | RTLD_LOCAL);
-            if (b->dl) break;
-            const char* e = dlerror();
-            errs += std::string("\n  ") + c + ": " + (e ? e : "?");
-        }
-        if (!b->dl) throw std::runtime_error("cannot load the model library " + dll + errs);
-        b->bind(b->create_from_json, "mmpc_create_from_json");
-        b->bind(b->destroy, "mmpc_destroy");
-        b->bind(b->get_model_info, "mmpc_get_model_info");
-        b->bind(b->solve_batch_host, "mmpc_solve_batch_host");
-        b->bind(b->last_error, "mmpc_last_error");
-        return b;
-    }
-};
+using detail::ModelLibrary;
 
 ModelControl::ModelControl(std::string model_name, std::vector<double> Q, std::vector<double> R,
                            std::vector<double> Rm, Dict solver_opts)
@@ -94,7 +41,7 @@ void ModelControl::load_model(const std::string& model_name) {
     model_parameters = model_parameters_from_json_string(ss.str());
     if (m_handle) m_backend->destroy(m_handle);
     m_handle = nullptr;
-    m_backend = Backend::load(model_parameters, path);
+    m_backend = ModelLibrary::load(model_parameters, path);
     m_backend->check(m_backend->create_from_json(ss.str().c_str(), nullptr, &m_handle), "mmpc_create");
     mmpc_model_info info;
     m_backend->check(m_backend->get_model_info(m_handle, &info), "mmpc_get_model_info");

@@ -75,6 +75,7 @@ def test_generated_linear_functions_casadi_abi(golden_kat, oracle, mmpc_mod, tmp
     external C ABI (src/codegen_usage.cpp:73-181) with ctypes: CasADi column-major outputs equal to the device
     linearisation bit for bit, and to the sympy K2/K3 fixtures (2-link, 1e-11) / the oracle (exo, 1e-12)."""
     import ctypes as C
+    mmpc_mod.lib()  # HIP runtime initialised as every caller in this process does it (torch first, mmpc.lib)
     subprocess.run(["make", "-s", "-C", HOST], check=True)
     out = subprocess.run([os.path.join(HOST, "bin", "host_selftest")], cwd=tmp_path, capture_output=True, text=True)
     assert out.returncode == 0, out.stdout + out.stderr
