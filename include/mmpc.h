@@ -139,6 +139,14 @@ int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_han
 int mmpc_destroy(mmpc_handle* h);
 int mmpc_get_model_info(const mmpc_handle* h, mmpc_model_info* info);
 int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts);
+/* State bounds x_lb <= x_k <= x_ub for k = 1..N ([nx] host arrays, NULL = unbounded; |b| >= 1e19 is infinite),
+ * the lbx/ubx IPOPT receives for the states (ModelControl.cpp:37-50,146-157).  A handle starts with the JSON's
+ * x_min/x_max (ModelParameters.cpp:66-69: +-10e30 -> +-inf).  Finite state bounds make the solves run the
+ * primal-dual interior-point variant (IPOPT-style barrier on the same Gauss-Newton model), which
+ * then also handles u_lb/u_ub; it needs a Riccati solver (AUTO never picks CONDENSED for it). */
+int mmpc_set_state_bounds(mmpc_handle* h, const double* x_lb, const double* x_ub);
+int mmpc_get_state_bounds(const mmpc_handle* h, double* x_lb, double* x_ub);
+
 /* Pre-allocate the Riccati solvers' device workspace for batches up to B (so that later
  * stream-ordered solves allocate nothing; the workspace grows on demand otherwise).  *bytes (may be NULL) receives the workspace size. */
 int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes);

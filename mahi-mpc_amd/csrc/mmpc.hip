@@ -71,6 +71,13 @@ struct mmpc_handle {
     double* ws = nullptr;
     size_t ws_bytes = 0;
     int ws_dev = -1;
+    // state bounds of x_1..x_N (JSON x_min/x_max, or mmpc_set_state_bounds); a device copy for the kernels
+    double x_lb[16], x_ub[16];
+    bool x_bounded = false;
+    std::mutex xb_mu;
+    double* d_xb = nullptr;  // [2][nx]
+    int d_xb_dev = -1;
+    bool d_xb_dirty = true;
 };
 
 namespace {
@@ -397,9 +404,9 @@ size_t group_workspace_bytes(const mmpc_model_info& mi, int64_t B) {
     return static_cast<size_t>(group_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) *
            static_cast<size_t>(B) * sizeof(double);
 }
-size_t group_lds_bytes(const mmpc_model_info& mi, int nq, bool bounded = true) {
-    return static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, nq, mi.num_shooting_nodes, bounded,
-                                                 mi.is_linear != 0)) * kGroupsPerWave *
+size_t group_lds_bytes(const mmpc_model_info& mi, int nq, bool bounded = true, bool xb = false) {
+    return static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, nq, mi.num_shooting_nodes, bounded && !xb,
+                                                 mi.is_linear != 0, xb)) * kGroupsPerWave *
            sizeof(double);
 }
 constexpr size_t kMaxGroupLds = 160 * 1024;  // gfx950: 160 KB of LDS per workgroup (attribute raised above 64 KB)
@@ -413,7 +420,17 @@ int set_dynamic_lds(K kernel, size_t bytes) {
 }
 
 // the KKT solver a solve of B instances runs (opts.kkt_solver, or the AUTO choice)
+int resolve_kkt_solver_base(const mmpc_handle* h, int64_t B);
 int resolve_kkt_solver(const mmpc_handle* h, int64_t B) {
+    const int s = resolve_kkt_solver_base(h, B);
+    // state bounds (interior-point variant): the Riccati solvers only
+    if (h->x_bounded && h->opts.kkt_solver == MMPC_KKT_AUTO && s == MMPC_KKT_CONDENSED) return MMPC_KKT_RICCATI_GROUP;
+    if (h->x_bounded && h->opts.kkt_solver == MMPC_KKT_AUTO && s == MMPC_KKT_RICCATI &&
+        group_lds_bytes(h->info, h->nq, false, true) <= kMaxGroupLds)
+        return MMPC_KKT_RICCATI_GROUP;  // until the lane kernel has the interior-point variant
+    return s;
+}
+int resolve_kkt_solver_base(const mmpc_handle* h, int64_t B) {
     const mmpc_model_info& mi = h->info;
     if (h->opts.kkt_solver != MMPC_KKT_AUTO) return h->opts.kkt_solver;
     if (h->opts.factor_fp32) return MMPC_KKT_RICCATI;
@@ -435,11 +452,38 @@ int resolve_kkt_solver(const mmpc_handle* h, int64_t B) {
     return MMPC_KKT_RICCATI;
 }
 
-template <class Model, bool BOUNDED>
+template <class Model, bool BOUNDED, bool XB = false>
 int launch_group(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const SolveParams& p, GroupWork gwk) {
-    int rc = set_dynamic_lds(sqp_group_kernel<Model, BOUNDED>, lds);
+    int rc = set_dynamic_lds(sqp_group_kernel<Model, BOUNDED, XB>, lds);
     if (rc) return rc;
-    sqp_group_kernel<Model, BOUNDED><<<grid, block, lds, stream>>>(p, gwk);
+    sqp_group_kernel<Model, BOUNDED, XB><<<grid, block, lds, stream>>>(p, gwk);
+    return MMPC_OK;
+}
+
+// the state bounds on the current device (synchronous upload when they changed or the device did)
+int ensure_state_bounds_device(mmpc_handle* h, const double** lb, const double** ub) {
+    int dev = -1;
+    MMPC_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(h->xb_mu);
+    const int nx = h->info.num_x;
+    if (!h->d_xb || h->d_xb_dev != dev) {
+        if (h->d_xb) MMPC_HIP(hipFree(h->d_xb));
+        h->d_xb = nullptr;
+        MMPC_HIP(hipMalloc(reinterpret_cast<void**>(&h->d_xb), 2 * nx * sizeof(double)));
+        h->d_xb_dev = dev;
+        h->d_xb_dirty = true;
+    }
+    if (h->d_xb_dirty) {
+        double hb[32];
+        for (int i = 0; i < nx; ++i) {
+            hb[i] = h->x_lb[i];
+            hb[nx + i] = h->x_ub[i];
+        }
+        MMPC_HIP(hipMemcpy(h->d_xb, hb, 2 * nx * sizeof(double), hipMemcpyHostToDevice));
+        h->d_xb_dirty = false;
+    }
+    *lb = h->d_xb;
+    *ub = h->d_xb + nx;
     return MMPC_OK;
 }
 
@@ -507,6 +551,11 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
     // points pass NULL for bounds that are all infinite
     const bool bounded = u_lb || u_ub;
+    p.x_lb = p.x_ub = nullptr;
+    if (h->x_bounded) {  // state bounds: the interior-point variant (sqp_wave.h "state bounds")
+        int rc = ensure_state_bounds_device(h, &p.x_lb, &p.x_ub);
+        if (rc) return rc;
+    }
     const int solver = resolve_kkt_solver(h, B);
     return launch_kernel(h, solver, p, bounded, stream);
 }
@@ -518,7 +567,8 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
     const int N = mi.num_shooting_nodes;
     if (solver == MMPC_KKT_RICCATI_GROUP) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 needs the lane Riccati solver");
-        const size_t lds = group_lds_bytes(mi, h->nq, bounded);
+        const bool xb = p.x_lb != nullptr;
+        const size_t lds = group_lds_bytes(mi, h->nq, bounded, xb);
         if (lds > kMaxGroupLds) return fail(MMPC_ERR_UNSUPPORTED, "group Riccati solver: stage data exceeds 160 KB LDS");
         LaneWork lw;
         int rc = ensure_workspace(h, B, &lw);
@@ -527,6 +577,7 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         dim3 grid(grid1d(B, kGroupsPerWave)), block(64);
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
+            if (xb) return launch_group<M, false, true>(grid, block, lds, stream, p, gwk);
             return bounded ? launch_group<M, true>(grid, block, lds, stream, p, gwk)
                            : launch_group<M, false>(grid, block, lds, stream, p, gwk);
         });
@@ -534,6 +585,8 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         MMPC_HIP(hipGetLastError());
         return MMPC_OK;
     }
+    if (p.x_lb && solver != MMPC_KKT_RICCATI_GROUP)
+        return fail(MMPC_ERR_UNSUPPORTED, "state bounds need a Riccati solver (MMPC_KKT_RICCATI_GROUP)");
     if (solver == MMPC_KKT_CONDENSED) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 is a Riccati-solver option");
 #if MMPC_BUILTIN_MODELS
@@ -622,6 +675,11 @@ int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_han
     if (!h) return fail(MMPC_ERR_INVALID_ARG, "out of memory");
     h->info = info;
     h->nq = model_nq(info.model_id);
+    for (int i = 0; i < info.num_x; ++i) {  // x_min/x_max of the JSON (ModelControl.cpp:37-50)
+        h->x_lb[i] = info.x_min[i];
+        h->x_ub[i] = info.x_max[i];
+        h->x_bounded |= info.x_min[i] > -1e19 || info.x_max[i] < 1e19;
+    }
     h->opts = o;
     *out = h;
     g_last_error.clear();
@@ -648,6 +706,10 @@ int mmpc_destroy(mmpc_handle* h) {
         DeviceGuard g(h->ws_dev);
         (void)hipFree(h->ws);
     }
+    if (h->d_xb) {
+        DeviceGuard g(h->d_xb_dev);
+        (void)hipFree(h->d_xb);
+    }
     delete h;
     return MMPC_OK;
 }
@@ -663,6 +725,31 @@ int mmpc_set_opts(mmpc_handle* h, const mmpc_opts* opts) {
     int rc = validate_opts(opts);
     if (rc) return rc;
     h->opts = *opts;
+    return MMPC_OK;
+}
+
+int mmpc_set_state_bounds(mmpc_handle* h, const double* x_lb, const double* x_ub) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->xb_mu);
+    bool any = false;
+    for (int i = 0; i < h->info.num_x; ++i) {
+        const double l = x_lb ? x_lb[i] : -INFINITY, u = x_ub ? x_ub[i] : INFINITY;
+        if (l != l || u != u || l > u) return fail(MMPC_ERR_INVALID_ARG, "state bounds: NaN or lower > upper");
+        h->x_lb[i] = l;
+        h->x_ub[i] = u;
+        any |= l > -1e19 || u < 1e19;
+    }
+    h->x_bounded = any;
+    h->d_xb_dirty = true;
+    return MMPC_OK;
+}
+
+int mmpc_get_state_bounds(const mmpc_handle* h, double* x_lb, double* x_ub) {
+    if (!h || !x_lb || !x_ub) return fail(MMPC_ERR_INVALID_ARG, "null argument");
+    for (int i = 0; i < h->info.num_x; ++i) {
+        x_lb[i] = h->x_lb[i];
+        x_ub[i] = h->x_ub[i];
+    }
     return MMPC_OK;
 }
 

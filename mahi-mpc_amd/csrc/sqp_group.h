@@ -27,10 +27,11 @@ constexpr int kGroupsPerWave = 4;
 // when used: at cfg#2 that keeps a 4-instance workgroup at 38.8 KB, so 4 workgroups (one per SIMD) fit a CU's
 // 160 KB; with them 41 KB leaves one SIMD of every CU idle (measured: 0.78 vs 0.6x ms).
 // nq = kinematic rows of the model (sqp_lane.h a_mul); the stage blocks are h da/dq, h da/dz, h da/du.
+// xb: the interior-point variant (state bounds) adds z_l, z_u, Sigma, b, z_u - z_l per stage for (x_{k+1} | u_k).
 __host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int nq, int N, bool bounded = true,
-                                                   bool linear = true) {
+                                                   bool linear = true, bool xb = false) {
     return N * (3 * nx + (nx - nq) * (nq + (nx - nq) + nu) + 2 * nu) + 3 * (N + 1) * nx + (bounded ? N * nu : 0) +
-           (linear ? (nx - nq) * (nq + (nx - nq) + nu) + nx : 0);
+           (linear ? (nx - nq) * (nq + (nx - nq) + nu) + nx : 0) + (xb ? 5 * N * (nx + nu) : 0);
 }
 // HBM workspace doubles per instance: K_k | kff_k per stage
 __host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) { return N * nu * (nx + nu + 1); }
@@ -42,6 +43,11 @@ struct GroupWork {
 __device__ __forceinline__ double group_sum(double v) {
 #pragma unroll
     for (int o = 8; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ double group_min(double v) {
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) v = fmin(v, __shfl_xor(v, o));
     return v;
 }
 __device__ __forceinline__ double group_max(double v) {
@@ -94,8 +100,11 @@ __device__ __forceinline__ void group_model(bool lin, const double* lFq, const d
     }
 }
 
-template <class Model, bool BOUNDED = false>
+// XB: state bounds (oracle solve_one_ip), the primal-dual interior-point variant for state AND control bounds;
+// BOUNDED: control bounds only (projected GN-SQP).  At most one of them.
+template <class Model, bool BOUNDED = false, bool XB = false>
 __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork gw) {
+    static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
     constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)
     constexpr int FQ = NA * NQ, FD = NA * NA, FU = NA * NU;  // stage block sizes (sqp_lane.h a_mul)
@@ -115,7 +124,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     const double h = p.h;
 
     // ---- LDS views of this instance ----
-    double* const sX = shm + gi * group_lds_doubles(NX, NU, NQ, N, BOUNDED, p.is_linear != 0);  // [N+1][NX]
+    double* const sX = shm + gi * group_lds_doubles(NX, NU, NQ, N, BOUNDED, p.is_linear != 0, XB);  // [N+1][NX]
     double* const sDX = sX + (N + 1) * NX;                         // [N+1][NX]
     double* const sD = sDX + (N + 1) * NX;                         // [N+1][NX]
     double* const sU = sD + (N + 1) * NX;                          // [N][NU]
@@ -128,6 +137,13 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const sR = sFu + N * FU;                               // [N][NX]      targets r_k
     double* const sHold = sR + N * NX;                             // [N][NU]      bound a control is held at
     double* const sLin = sHold + (BOUNDED ? N * NU : 0);           // linear mode: Fq | Fqd | Fu | xdot
+    // interior point (XB): per stage k, y = (x_{k+1} | u_k) [NY]: duals z_l, z_u, Sigma, b, z_u - z_l
+    constexpr int NY = NX + NU;
+    double* const sZl = sLin + (p.is_linear ? FQ + FD + FU + NX : 0);  // [N][NY]
+    double* const sZu = sZl + N * NY;
+    double* const sSg = sZu + N * NY;
+    double* const sBb = sSg + N * NY;
+    double* const sZg = sBb + N * NY;
     double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
     const double* const trg = p.traj + ii * (int64_t)N * NX;
 
@@ -159,6 +175,22 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         }
     }
     const double* const tr = sR;
+    double yl[XB ? NY : 1], yu[XB ? NY : 1];
+    double mub = kIpMu0;  // barrier parameter (f = J/2 scale)
+    if constexpr (XB) {
+        load_ip_bounds<NX, NU>(p, yl, yu);
+        __builtin_amdgcn_wave_barrier();
+        // y pushed into the interior, z = 1 on finite bounds (oracle solve_one_ip)
+        for (int k = gl; k < N; k += G) {
+#pragma unroll
+            for (int j = 0; j < NY; ++j) {
+                double& y = j < NX ? sX[(k + 1) * NX + j] : sU[k * NU + j - NX];
+                y = ip_push(y, yl[j], yu[j]);
+                sZl[k * NY + j] = yl[j] > -INFINITY ? 1.0 : 0.0;
+                sZu[k * NY + j] = yu[j] < INFINITY ? 1.0 : 0.0;
+            }
+        }
+    }
     // linear mode: acceleration Jacobians and xdot at (x_0, u_prev) (ModelControl.cpp:125-135), in LDS (keeps
     // 20-64 VGPRs free for the serial Riccati sweep); the linearisation point x_0 is sX[0..NX) (pinned)
     const bool lin = p.is_linear != 0;
@@ -226,6 +258,24 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 J0 = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], J0));
             }
         }
+        double lsum = 0.0, cmpl0 = 0.0, cmplmu = 0.0;  // interior point: sum log s, max |s z|, max |s z - mu|
+        if constexpr (XB) {
+            for (int k = gl; k < N; k += G) {
+#pragma unroll
+                for (int j = 0; j < NY; ++j) {
+                    const double y = j < NX ? sX[(k + 1) * NX + j] : sU[k * NU + j - NX];
+                    double sg, bb, zg;
+                    ip_terms(y, yl[j], yu[j], sZl[k * NY + j], sZu[k * NY + j], mub, sg, bb, zg, cmpl0, cmplmu, lsum);
+                    sSg[k * NY + j] = sg;
+                    sBb[k * NY + j] = bb;
+                    sZg[k * NY + j] = zg;
+                }
+            }
+            lsum = group_sum(lsum);
+            cmpl0 = group_max(cmpl0);
+            cmplmu = group_max(cmplmu);
+            nonfinite |= !isfinite(lsum);
+        }
         J0 = group_sum(J0);
         c1 = group_sum(c1);
         cmax = group_max(cmax);
@@ -253,6 +303,11 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 const double eb = sX[N * NX + r] - tr[(N - 1) * NX + r];  // x_N - r_{N-1}
                 pv[r] = Q[r] * eb;
                 lam[r] = Q[r] * (sD[N * NX + r] + eb);  // lam_N = Q e_{N-1}
+                if constexpr (XB) {  // barrier at x_N: Sigma, b in the value function, z_u - z_l in the adjoint
+                    P[r][r] += sSg[(N - 1) * NY + r];
+                    pv[r] += sBb[(N - 1) * NY + r];
+                    lam[r] += sZg[(N - 1) * NY + r];
+                }
                 lmax = fmax(lmax, fabs(lam[r]));
             }
 #pragma unroll
@@ -281,6 +336,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     for (int s = 0; s < NA; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
                     g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
                     if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
+                    if (XB) g += sZg[k * NY + NX + c];  // reduced Lagrangian gradient
                     if (!BOUNDED) {
                         gmax = fmax(gmax, fabs(2.0 * g));
                     } else {  // projected gradient; hold rule (pass 0) or the holds of the previous solve
@@ -304,6 +360,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         lam[r] = fma(Q[r], sD[k * NX + r] + x[r] - tr[(k - 1) * NX + r], ln[r]);
+                        if (XB) lam[r] += sZg[(k - 1) * NY + r];
                         lmax = fmax(lmax, fabs(lam[r]));
                     }
                 }
@@ -336,9 +393,11 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         for (int s = 0; s < NA; ++s)
                             t = fma(hFu[s * NU + a], Gm[NQ + s][b], fma(Ps(NQ + s, NX + a), hFu[s * NU + b], t));
                         if (a == b) t += R[a] + Rm[a];
+                        if (XB && a == b) t += sSg[k * NY + NX + a];
                         Hww[a][b] = t;
                     }
                     double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
+                    if (XB) t += sBb[k * NY + NX + a];
 #pragma unroll
                     for (int s = 0; s < NA; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
 #pragma unroll
@@ -409,12 +468,16 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         }
                         at_mul<NQ, NA, double>(h, hFq, hFqd, tcol, row);
 #pragma unroll
-                        for (int a = 0; a <= b; ++a) Pn[a][b] = row[a] + ((a == b) ? Q[a] : 0.0);
+                        for (int a = 0; a <= b; ++a)
+                            Pn[a][b] = row[a] + ((a == b) ? Q[a] + (XB ? sSg[(k - 1) * NY + a] : 0.0) : 0.0);
                     }
                     double t[NX];
                     at_mul<NQ, NA, double>(h, hFq, hFqd, mv, t);
 #pragma unroll
-                    for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - tr[(k - 1) * NX + q], t[q]);
+                    for (int q = 0; q < NX; ++q) {
+                        pn[q] = fma(Q[q], x[q] - tr[(k - 1) * NX + q], t[q]);
+                        if (XB) pn[q] += sBb[(k - 1) * NY + q];
+                    }
 #pragma unroll
                     for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
                 }
@@ -422,7 +485,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 // update of P~ and p~.  nu = 2: explicit inverse (one reciprocal; no square roots -- the serial
                 // sweep is latency-bound); otherwise Cholesky, Y = L^-1 Z.
                 double Kt[NU][NS + 1];
-                if constexpr (NU == 2) {
+                if constexpr (NU == 2 && !XB) {  // XB: Cholesky (Y^T Y stays PSD with the large barrier Sigma)
                     const double det = fma(Hww[0][0], Hww[1][1], -Hww[0][1] * Hww[0][1]);
                     fact_ok &= (Hww[0][0] > 0.0) && (det > 0.0) && isfinite(det);
                     const double idet = rcp_nr(det);  // two Newton steps: ~1 ulp, off the division's long chain
@@ -481,7 +544,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 if (k == 0) break;
                 // P~_k = blkdiag(A^T P_xx A + Q, R) - Z^T H_ww^-1 Z, p~_k = pn - Z^T H_ww^-1 h_w:
                 // nu = 2 as Y^T Kt (Y = Z, Kt = H_ww^-1 Z), Cholesky as Y^T Y (Y = L^-1 Z)
-                const double(&YB)[NU][NS + 1] = (NU == 2) ? Kt : Y;
+                const double(&YB)[NU][NS + 1] = (NU == 2 && !XB) ? Kt : Y;
 #pragma unroll
                 for (int a = 0; a < NS; ++a) {
                     double t = pn[a];
@@ -650,6 +713,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         MMPC_PHASE(2);
         nonfinite = (group_max((double)nonfinite) != 0.0);
         kkt = fmax(gmax, cmax);
+        if (XB) kkt = fmax(kkt, 2.0 * cmpl0);  // J-scale complementarity
         double* trc = p.trace && valid ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
         if (trc && gl == 0) {
             trc[0] = gmax;
@@ -662,7 +726,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             status = ST_NONFINITE;
             break;
         }
-        if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
+        if (gmax <= p.tol_grad && cmax <= p.tol_defect && (!XB || 2.0 * cmpl0 <= kIpTolCompl)) {
             status = ST_CONVERGED;
             break;
         }
@@ -675,6 +739,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             break;
         }
         if (BOUNDED) pg_prev = gmax;
+        // barrier update for the next iteration (IPOPT monotone rule, lagged; oracle solve_one_ip)
+        const double mub_next = (XB && fmax(fmax(0.5 * gmax, cmax), cmplmu) <= kIpKappaEps * mub)
+                                    ? fmax(kIpTolCompl / 20.0, fmin(kIpKappaMu * mub, pow(mub, kIpThetaMu)))
+                                    : mub;
 
         MMPC_PHASE(3);
         if (gl == 0) {
@@ -694,15 +762,32 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         dJ = group_bcast(dJ, gbase);
         __builtin_amdgcn_wave_barrier();
         MMPC_PHASE(4);
+        // interior point: fraction to the boundary (primal alpha_max, dual alpha_z), barrier directional derivative
+        double amax = 1.0, az = 1.0, dbar = 0.0;
+        if constexpr (XB) {
+            const double tau = kIpTau;
+            for (int k = gl; k < N; k += G) {
+#pragma unroll
+                for (int j = 0; j < NY; ++j) {
+                    const double y = j < NX ? sX[(k + 1) * NX + j] : sU[k * NU + j - NX];
+                    const double dy = j < NX ? sDX[(k + 1) * NX + j] : sDU[k * NU + j - NX];
+                    ip_step_limits(y, dy, yl[j], yu[j], sZl[k * NY + j], sZu[k * NY + j], mub, tau, sBb[k * NY + j],
+                                   amax, az, dbar);
+                }
+            }
+            amax = group_min(amax);
+            az = group_min(az);
+            dbar = group_sum(dbar);
+        }
 
         // ---- D. stage-parallel l1-merit Armijo line search (noise-aware, as sqp_wave.h), update ----
         mu = fmax(mu, 4.0 * lmax + 1.0);
-        const double phi0 = fma(mu, c1, J0);
-        const double dphi = dJ - mu * c1;
-        double alpha = 1.0;
+        const double phi0 = XB ? fma(mu, c1, fma(-2.0 * mub, lsum, J0)) : fma(mu, c1, J0);
+        const double dphi = XB ? dJ + dbar - mu * c1 : dJ - mu * c1;
+        double alpha = amax;
         bool accepted = false;
         for (int ls = 0; ls < 30; ++ls) {
-            double Jt = 0.0, ct = 0.0;
+            double Jt = 0.0, ct = 0.0, lt = 0.0;
             for (int k = gl; k < N; k += G) {
                 double x[NX], u[NU], xd[NX];
 #pragma unroll
@@ -727,10 +812,18 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     const double dif = u[c] - um;
                     Jt = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], Jt));
                 }
+                if constexpr (XB) {
+#pragma unroll
+                    for (int j = 0; j < NY; ++j) {
+                        const double y = j < NX ? fma(alpha, sDX[(k + 1) * NX + j], sX[(k + 1) * NX + j]) : u[j - NX];
+                        lt += ip_log_slacks(y, yl[j], yu[j]);
+                    }
+                }
             }
             Jt = group_sum(Jt);
             ct = group_sum(ct);
-            const double phit = fma(mu, ct, Jt);
+            if (XB) lt = group_sum(lt);
+            const double phit = XB ? fma(mu, ct, fma(-2.0 * mub, lt, Jt)) : fma(mu, ct, Jt);
             const double noise = 1.0 + fabs(phi0);
             if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) {
                 accepted = true;
@@ -739,9 +832,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             alpha *= 0.5;
         }
         if (trc && gl == 0) {
-            trc[4] = dJ;
+            trc[4] = XB ? amax : dJ;
             trc[5] = alpha;
-            trc[6] = mu;
+            trc[6] = XB ? mub : mu;
+            if (XB) trc[3] = cmpl0;
         }
         MMPC_PHASE(5);
         if (!accepted) {
@@ -749,16 +843,32 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             break;
         }
         __builtin_amdgcn_wave_barrier();
-        for (int k = gl; k <= N; k += G) {
-            if (k > 0) {
+        if constexpr (XB) {  // y and the duals of stage k's (x_{k+1} | u_k), as oracle solve_one_ip
+            for (int k = gl; k < N; k += G) {
 #pragma unroll
-                for (int r = 0; r < NX; ++r) sX[k * NX + r] = fma(alpha, sDX[k * NX + r], sX[k * NX + r]);
+                for (int j = 0; j < NY; ++j) {
+                    double& y = j < NX ? sX[(k + 1) * NX + j] : sU[k * NU + j - NX];
+                    const double dy = j < NX ? sDX[(k + 1) * NX + j] : sDU[k * NU + j - NX];
+                    double zl = sZl[k * NY + j], zu = sZu[k * NY + j], yn;
+                    ip_update(y, dy, yl[j], yu[j], zl, zu, mub, alpha, az, yn);
+                    y = yn;
+                    sZl[k * NY + j] = zl;
+                    sZu[k * NY + j] = zu;
+                }
             }
-            if (k < N) {
+            mub = mub_next;
+        } else {
+            for (int k = gl; k <= N; k += G) {
+                if (k > 0) {
 #pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    const double un = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
-                    sU[k * NU + c] = BOUNDED ? proj(un, lbv[c], ubv[c]) : un;
+                    for (int r = 0; r < NX; ++r) sX[k * NX + r] = fma(alpha, sDX[k * NX + r], sX[k * NX + r]);
+                }
+                if (k < N) {
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {
+                        const double un = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
+                        sU[k * NU + c] = BOUNDED ? proj(un, lbv[c], ubv[c]) : un;
+                    }
                 }
             }
         }

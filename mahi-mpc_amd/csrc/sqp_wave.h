@@ -46,6 +46,8 @@ struct SolveParams {
     int64_t w_stride;
     const double* u_lb;
     const double* u_ub;
+    const double* x_lb;  // state bounds of x_1..x_N [nx] (ModelControl.cpp:37-50), or nullptr: interior point
+    const double* x_ub;
     double* V;
     int32_t* status;
     int32_t* iters;
@@ -83,6 +85,105 @@ __device__ __forceinline__ void load_bounds(const SolveParams& p, double* lbv, d
             if (p.u_ub && p.u_ub[c] < 1e19) ubv[c] = p.u_ub[c];
         }
     }
+}
+
+// ---------------- state bounds: primal-dual interior point (oracle/mmpc_oracle.c solve_one_ip) ----------------
+// With finite state bounds the Riccati kernels run the XB variant: barrier problem min f - mu sum log s on f = J/2
+// for the state AND control bounds, Sigma = z_l/s_l + z_u/s_u and b = -mu/s_l + mu/s_u added to the Riccati
+// stage blocks, fraction-to-the-boundary steps, l1 merit with the barrier term, mu updated (lagged) when
+// E_mu <= 10 mu.  The constants are IPOPT's defaults (mu_init, kappa_eps, kappa_mu, theta_mu, bound_push,
+// kappa_Sigma).
+constexpr double kIpMu0 = 0.1, kIpKappaEps = 10.0, kIpKappaMu = 0.2, kIpThetaMu = 1.5, kIpPush = 1e-2,
+                 kIpKappaSigma = 1e10;
+// complementarity tolerance 2 max s z (J-scale), barrier floor kIpTolCompl / 20 and a constant fraction to the
+// boundary (oracle IP_TOL_COMPL, IP_TAU): keep Sigma = z/s where the Riccati Schur complements stay positive
+// definite (IPOPT: compl_inf_tol 1e-4, tau = max(0.99, 1 - mu))
+constexpr double kIpTolCompl = 1e-8, kIpTau = 0.99;
+// y pushed inside [l, u] (IPOPT bound_push / bound_frac): by 1e-2 max(1, |bound|), at most 1e-2 of the box
+__device__ __forceinline__ double ip_push(double y, double l, double u) {
+    const double pl = (l > -INFINITY) ? fmin(kIpPush * fmax(1.0, fabs(l)), (u < INFINITY) ? kIpPush * (u - l) : INFINITY) : 0.0;
+    const double pu = (u < INFINITY) ? fmin(kIpPush * fmax(1.0, fabs(u)), (l > -INFINITY) ? kIpPush * (u - l) : INFINITY) : 0.0;
+    if (l > -INFINITY && y < l + pl) y = l + pl;
+    if (u < INFINITY && y > u - pu) y = u - pu;
+    return y;
+}
+// bounds of y = (x_{k+1} [nx] | u_k [nu]) of a stage: |b| >= 1e19 is infinite
+template <int NX, int NU>
+__device__ __forceinline__ void load_ip_bounds(const SolveParams& p, double* yl, double* yu) {
+#pragma unroll
+    for (int j = 0; j < NX + NU; ++j) {
+        const double* lo = j < NX ? p.x_lb : p.u_lb;
+        const double* hi = j < NX ? p.x_ub : p.u_ub;
+        const int i = j < NX ? j : j - NX;
+        yl[j] = (lo && lo[i] > -1e19) ? lo[i] : -INFINITY;
+        yu[j] = (hi && hi[i] < 1e19) ? hi[i] : INFINITY;
+    }
+}
+// barrier pieces of one bounded variable (oracle solve_one_ip): Sigma, b, zu - zl, complementarity, log slacks
+__device__ __forceinline__ void ip_terms(double y, double l, double u, double zl, double zu, double mub, double& sg,
+                                         double& bb, double& zg, double& c0, double& cmu, double& lg) {
+    sg = 0.0;
+    bb = 0.0;
+    zg = 0.0;
+    if (l > -INFINITY) {
+        const double sl = y - l;
+        sg += zl / sl;
+        bb -= mub / sl;
+        zg -= zl;
+        c0 = fmax(c0, fabs(sl * zl));
+        cmu = fmax(cmu, fabs(sl * zl - mub));
+        lg += log(sl);
+    }
+    if (u < INFINITY) {
+        const double su = u - y;
+        sg += zu / su;
+        bb += mub / su;
+        zg += zu;
+        c0 = fmax(c0, fabs(su * zu));
+        cmu = fmax(cmu, fabs(su * zu - mub));
+        lg += log(su);
+    }
+}
+// fraction to the boundary (tau) of a primal step dy and of the dual steps it implies; dbar += 2 b dy (J-scale)
+__device__ __forceinline__ void ip_step_limits(double y, double dy, double l, double u, double zl, double zu,
+                                               double mub, double tau, double bb, double& amax, double& az,
+                                               double& dbar) {
+    if (l > -INFINITY) {
+        const double sl = y - l;
+        if (dy < 0.0) amax = fmin(amax, -tau * sl / dy);
+        const double dz = mub / sl - zl - zl / sl * dy;
+        if (dz < 0.0) az = fmin(az, -tau * zl / dz);
+    }
+    if (u < INFINITY) {
+        const double su = u - y;
+        if (dy > 0.0) amax = fmin(amax, tau * su / dy);
+        const double dz = mub / su - zu + zu / su * dy;
+        if (dz < 0.0) az = fmin(az, -tau * zu / dz);
+    }
+    dbar = fma(2.0 * bb, dy, dbar);
+}
+// dual update z + alpha_z dz (dz at the old point), then the kappa_Sigma safeguard at the new point y + alpha dy
+__device__ __forceinline__ void ip_update(double y, double dy, double l, double u, double& zl, double& zu, double mub,
+                                          double alpha, double az, double& ynew) {
+    ynew = fma(alpha, dy, y);
+    if (l > -INFINITY) {
+        const double sl = y - l;
+        zl += az * (mub / sl - zl - zl / sl * dy);
+        const double sn = ynew - l;
+        zl = fmax(fmin(zl, kIpKappaSigma * mub / sn), mub / (kIpKappaSigma * sn));
+    }
+    if (u < INFINITY) {
+        const double su = u - y;
+        zu += az * (mub / su - zu + zu / su * dy);
+        const double sn = u - ynew;
+        zu = fmax(fmin(zu, kIpKappaSigma * mub / sn), mub / (kIpKappaSigma * sn));
+    }
+}
+__device__ __forceinline__ double ip_log_slacks(double y, double l, double u) {
+    double lg = 0.0;
+    if (l > -INFINITY) lg += log(y - l);
+    if (u < INFINITY) lg += log(u - y);
+    return lg;
 }
 
 // ---------------- wave helpers ----------------

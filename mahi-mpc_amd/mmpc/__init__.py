@@ -106,6 +106,8 @@ def lib(path: str | None = None):
         L.mmpc_nlp_eval_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 3
         L.mmpc_synth_batch.argtypes = [_vp, C.c_uint64, C.c_int64, C.c_int64] + [_vp] * 4
         L.mmpc_resolve_kkt_solver.argtypes = [_vp, C.c_int64, C.POINTER(C.c_int32)]
+        L.mmpc_set_state_bounds.argtypes = [_vp, _vp, _vp]
+        L.mmpc_get_state_bounds.argtypes = [_vp, _vp, _vp]
         L.mmpc_status_string.argtypes = [C.c_int32]
         L.mmpc_status_string.restype = C.c_char_p
         L.mmpc_last_error.restype = C.c_char_p
@@ -274,6 +276,17 @@ class Solver:
         self._check(self._L.mmpc_solve_batch_host(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights), ws,
                                            _ptr(lb), _ptr(ub), _ptr(V), _ptr(st), _ptr(it), _ptr(kkt)))
         return dict(V=V, status=st, iters=it, kkt=kkt)
+
+    def set_state_bounds(self, x_lb=None, x_ub=None):
+        """x_lb <= x_k <= x_ub for k = 1..N (None = unbounded); finite bounds select the interior-point variant."""
+        lb = None if x_lb is None else _f64(x_lb, (self.nx,))
+        ub = None if x_ub is None else _f64(x_ub, (self.nx,))
+        self._check(self._L.mmpc_set_state_bounds(self._h, _ptr(lb), _ptr(ub)))
+
+    def state_bounds(self):
+        lb, ub = np.zeros(self.nx), np.zeros(self.nx)
+        self._check(self._L.mmpc_get_state_bounds(self._h, _ptr(lb), _ptr(ub)))
+        return lb, ub
 
     def kkt_solver_for(self, B: int) -> int:
         """KKT_* solver a solve of B instances runs (the AUTO choice resolved)."""

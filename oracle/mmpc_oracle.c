@@ -616,12 +616,333 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
     return status;
 }
 
+/* ---------------- state bounds: primal-dual interior point (IPOPT-style) on the same GN model ----------------
+ * The reference hands x_min/x_max to IPOPT as lbx/ubx of x_1..x_N (ModelControl.cpp:37-50,146-157) -- IPOPT is a
+ * primal-dual barrier method (Waechter & Biegler 2006).  With finite state bounds the build runs the same kind of
+ * method on its Gauss-Newton model, for the state AND control bounds of the instance (the projected method of
+ * solve_one covers control-only bounds):
+ *   f = J/2 (the H, g of solve_one), barrier problem  min f - mu sum log s,  s = y - l | u - y  (finite bounds);
+ *   step: (H + Sigma) on the multiple-shooting variables, Sigma = z_l/s_l + z_u/s_u, gradient g - mu/s_l + mu/s_u,
+ *         condensed: Hc = H + Sigma_U + G^T Sigma_X G, gc = g + b_U + G^T (b_X + Sigma_X d);
+ *   dz_l = mu/s_l - z_l - (z_l/s_l) dy,  dz_u = mu/s_u - z_u + (z_u/s_u) dy;
+ *   fraction to the boundary tau = 0.99 for the primal (alpha_max) and dual (alpha_z) steps;
+ *   l1-merit Armijo backtracking from alpha_max on  J - 2 mu sum log s + nu |c|_1  (J-scale, as solve_one);
+ *   z safeguard  z in [mu / (1e10 s), 1e10 mu / s]  (IPOPT kappa_Sigma);
+ *   KKT error E_mu = max(|g + G^T(z_ux - z_lx) + z_uu - z_lu|, |c|, |s z - mu|); the barrier parameter is
+ *   updated after the step when E_mu <= 10 mu:  mu <- max(tol_c/20, min(0.2 mu, mu^1.5))  (IPOPT monotone rule,
+ *   lagged one iteration so that the Riccati kernels can fuse the test into their backward sweep);
+ *   start: mu = 0.1, z = 1, y pushed 1e-2 max(1, |bound|) (at most 1e-2 of the box) inside its bounds;
+ *   stop: 2|reduced Lagrangian gradient| <= tol_grad, |c| <= tol_defect, 2 max s z <= IP_TOL_COMPL (J-scale). */
+#define IP_MU0 0.1
+#define IP_KAPPA_EPS 10.0
+#define IP_KAPPA_MU 0.2
+#define IP_THETA_MU 1.5
+#define IP_PUSH 1e-2
+#define IP_KAPPA_SIGMA 1e10
+/* complementarity tolerance (J-scale, 2 max s z; IPOPT's default compl_inf_tol is 1e-4) and a constant fraction
+ * to the boundary tau = 0.99 (IPOPT: max(0.99, 1 - mu), which near the solution lets a slack collapse by a factor
+ * mu in one step): together they keep Sigma = z/s near z^2/mu_final ~ 1e12 -- the Riccati kernels' Schur
+ * complements lose positive definiteness to cancellation once Sigma reaches ~1e15 */
+#define IP_TOL_COMPL 1e-8
+#define IP_TAU 0.99
+
+static double ip_push(double y, double l, double u) {
+    const double pl = (l > -INFINITY) ? fmin(IP_PUSH * fmax(1.0, fabs(l)), (u < INFINITY) ? IP_PUSH * (u - l) : INFINITY) : 0.0;
+    const double pu = (u < INFINITY) ? fmin(IP_PUSH * fmax(1.0, fabs(u)), (l > -INFINITY) ? IP_PUSH * (u - l) : INFINITY) : 0.0;
+    if (l > -INFINITY && y < l + pl) y = l + pl;
+    if (u < INFINITY && y > u - pu) y = u - pu;
+    return y;
+}
+
+static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_prev, const double* traj,
+                        const double* w, const double* u_lb, const double* u_ub, const double* x_lb,
+                        const double* x_ub, int max_iter, double tol_grad, double tol_defect, double* V,
+                        int32_t* iters_out, double* kkt_out, double* J_out) {
+    const int N = s->N, M = s->M, S = N * NX;
+    const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
+    double lx[ORACLE_MAX_NX], ux[ORACLE_MAX_NX], lu[ORACLE_MAX_NU], uu[ORACLE_MAX_NU];
+    for (int r = 0; r < NX; ++r) {
+        lx[r] = (x_lb && x_lb[r] > -1e19) ? x_lb[r] : -INFINITY;
+        ux[r] = (x_ub && x_ub[r] < 1e19) ? x_ub[r] : INFINITY;
+    }
+    for (int q = 0; q < NU; ++q) {
+        lu[q] = (u_lb && u_lb[q] > -1e19) ? u_lb[q] : -INFINITY;
+        uu[q] = (u_ub && u_ub[q] < 1e19) ? u_ub[q] : INFINITY;
+    }
+    /* y = (X_1..X_N | U): bounds, duals, Sigma, barrier gradient b, steps */
+    const int NY = S + M;
+    double* yl = calloc((size_t)NY, sizeof(double));
+    double* yu = calloc((size_t)NY, sizeof(double));
+    double* zl = calloc((size_t)NY, sizeof(double));
+    double* zu = calloc((size_t)NY, sizeof(double));
+    double* sg = calloc((size_t)NY, sizeof(double));
+    double* bb = calloc((size_t)NY, sizeof(double));
+    double* zg = calloc((size_t)NY, sizeof(double));
+    double* dy = calloc((size_t)NY, sizeof(double));
+    double* tv = calloc((size_t)S, sizeof(double));
+    for (int i = 0; i < S; ++i) { yl[i] = lx[i % NX]; yu[i] = ux[i % NX]; }
+    for (int a = 0; a < M; ++a) { yl[S + a] = lu[a % NU]; yu[S + a] = uu[a % NU]; }
+#define YV(i) ((i) < S ? s->X[NX + (i)] : s->U[(i) - S])
+    for (int k = 0; k < N; ++k) {
+        memcpy(s->X + k * NX, V + k * ND, sizeof(double) * NX);
+        memcpy(s->U + k * NU, V + k * ND + NX, sizeof(double) * NU);
+    }
+    memcpy(s->X + N * NX, V + N * ND, sizeof(double) * NX);
+    memcpy(s->X, x0, sizeof(double) * NX);
+    for (int i = 0; i < NY; ++i) {
+        double* p = (i < S) ? &s->X[NX + i] : &s->U[i - S];
+        *p = ip_push(*p, yl[i], yu[i]);
+        zl[i] = (yl[i] > -INFINITY) ? 1.0 : 0.0;
+        zu[i] = (yu[i] < INFINITY) ? 1.0 : 0.0;
+    }
+    double mu_b = IP_MU0;  /* barrier parameter (f-scale) */
+    int status = ORACLE_MAX_ITER, it = 0;
+    double kkt = INFINITY, nu_pen = 0.0;
+    for (it = 0; it <= max_iter; ++it) {
+        for (int k = 0; k < N; ++k)
+            euler_step(h, s->X + k * NX, s->U + k * NU, s->F + k * NX, s->Ad + k * NX * NX, s->Bd + k * NX * NU);
+        double cmax = 0.0;
+        for (int i = 0; i < S; ++i) {
+            s->c[i] = s->F[i] - s->X[NX + i];
+            if (fabs(s->c[i]) > cmax || s->c[i] != s->c[i]) cmax = fabs(s->c[i]);
+        }
+        memset(s->d, 0, sizeof(double) * NX);
+        for (int k = 0; k < N; ++k)
+            for (int r = 0; r < NX; ++r) {
+                double ad = 0.0;
+                for (int q = 0; q < NX; ++q) ad += s->Ad[k * NX * NX + r * NX + q] * s->d[k * NX + q];
+                s->d[(k + 1) * NX + r] = ad + s->c[k * NX + r];
+                s->e[k * NX + r] = s->F[k * NX + r] + ad - traj[k * NX + r];
+            }
+        memset(s->G, 0, sizeof(double) * (size_t)S * M);
+        for (int j = 0; j < N; ++j) {
+            double col[ORACLE_MAX_NX][ORACLE_MAX_NU], nxt[ORACLE_MAX_NX][ORACLE_MAX_NU];
+            for (int r = 0; r < NX; ++r) for (int q = 0; q < NU; ++q) col[r][q] = s->Bd[j * NX * NU + r * NU + q];
+            for (int k = j; k < N; ++k) {
+                if (k > j) {
+                    for (int r = 0; r < NX; ++r) for (int q = 0; q < NU; ++q) {
+                        double t = 0.0;
+                        for (int p2 = 0; p2 < NX; ++p2) t += s->Ad[k * NX * NX + r * NX + p2] * col[p2][q];
+                        nxt[r][q] = t;
+                    }
+                    memcpy(col, nxt, sizeof col);
+                }
+                for (int r = 0; r < NX; ++r) for (int q = 0; q < NU; ++q)
+                    s->G[(size_t)(k * NX + r) * M + j * NU + q] = col[r][q];
+            }
+        }
+        for (int a = 0; a < M; ++a) {
+            for (int b = 0; b <= a; ++b) {
+                double t = 0.0;
+                for (int i = 0; i < S; ++i) t += s->G[(size_t)i * M + a] * Q[i % NX] * s->G[(size_t)i * M + b];
+                s->H[a * M + b] = t;
+                s->H[b * M + a] = t;
+            }
+            double t = 0.0;
+            for (int i = 0; i < S; ++i) t += s->G[(size_t)i * M + a] * Q[i % NX] * s->e[i];
+            s->g[a] = t;
+        }
+        for (int k = 0; k < N; ++k)
+            for (int q = 0; q < NU; ++q) {
+                int a = k * NU + q;
+                double um = (k == 0) ? u_prev[q] : s->U[(k - 1) * NU + q];
+                s->H[a * M + a] += R[q] + Rm[q];
+                s->g[a] += R[q] * (s->U[a] - um) + Rm[q] * s->U[a];
+                if (k + 1 < N) {
+                    s->H[a * M + a] += R[q];
+                    s->H[a * M + a + NU] -= R[q];
+                    s->H[(a + NU) * M + a] -= R[q];
+                    s->g[a] -= R[q] * (s->U[a + NU] - s->U[a]);
+                }
+            }
+        /* barrier pieces at y: Sigma, b = -mu/s_l + mu/s_u, z_u - z_l, complementarity */
+        double cmpl0 = 0.0, cmplmu = 0.0, logsum = 0.0;
+        for (int i = 0; i < NY; ++i) {
+            const double y = YV(i);
+            sg[i] = 0.0; bb[i] = 0.0; zg[i] = 0.0;
+            if (yl[i] > -INFINITY) {
+                const double sl = y - yl[i];
+                sg[i] += zl[i] / sl; bb[i] -= mu_b / sl; zg[i] -= zl[i];
+                cmpl0 = fmax(cmpl0, fabs(sl * zl[i])); cmplmu = fmax(cmplmu, fabs(sl * zl[i] - mu_b));
+                logsum += log(sl);
+            }
+            if (yu[i] < INFINITY) {
+                const double su = yu[i] - y;
+                sg[i] += zu[i] / su; bb[i] += mu_b / su; zg[i] += zu[i];
+                cmpl0 = fmax(cmpl0, fabs(su * zu[i])); cmplmu = fmax(cmplmu, fabs(su * zu[i] - mu_b));
+                logsum += log(su);
+            }
+        }
+        /* reduced Lagrangian gradient gz = g + G^T zg_X + zg_U */
+        double gzmax = 0.0;
+        for (int a = 0; a < M; ++a) {
+            double t = s->g[a] + zg[S + a];
+            for (int i = 0; i < S; ++i) t += s->G[(size_t)i * M + a] * zg[i];
+            if (fabs(t) > gzmax || t != t) gzmax = fabs(t);
+        }
+        kkt = fmax(fmax(2.0 * gzmax, cmax), 2.0 * cmpl0);
+        if (!isfinite(kkt)) { status = ORACLE_NONFINITE; break; }
+        if (2.0 * gzmax <= tol_grad && cmax <= tol_defect && 2.0 * cmpl0 <= IP_TOL_COMPL) { status = ORACLE_CONVERGED; break; }
+        if (it == max_iter) { status = ORACLE_MAX_ITER; break; }
+        const double e_mu = fmax(fmax(gzmax, cmax), cmplmu);
+        const double mu_next = (e_mu <= IP_KAPPA_EPS * mu_b)
+                                   ? fmax(IP_TOL_COMPL / 20.0, fmin(IP_KAPPA_MU * mu_b, pow(mu_b, IP_THETA_MU)))
+                                   : mu_b;
+        /* adjoint (penalty weight, as solve_one) */
+        for (int r = 0; r < NX; ++r) s->lam[N * NX + r] = Q[r] * s->e[(N - 1) * NX + r];
+        double lmax = 0.0;
+        for (int r = 0; r < NX; ++r) if (fabs(s->lam[N * NX + r]) > lmax) lmax = fabs(s->lam[N * NX + r]);
+        for (int k = N - 1; k >= 1; --k)
+            for (int r = 0; r < NX; ++r) {
+                double t = Q[r] * s->e[(k - 1) * NX + r];
+                for (int p2 = 0; p2 < NX; ++p2) t += s->Ad[k * NX * NX + p2 * NX + r] * s->lam[(k + 1) * NX + p2];
+                s->lam[k * NX + r] = t;
+                if (fabs(t) > lmax) lmax = fabs(t);
+            }
+        /* condensed barrier Newton step: Hc = H + Sigma_U + G^T Sigma_X G, gc = g + b_U + G^T (b_X + Sigma_X d) */
+        for (int i = 0; i < S; ++i) tv[i] = bb[i] + sg[i] * s->d[NX + i];
+        for (int a = 0; a < M; ++a) {
+            for (int b = 0; b <= a; ++b) {
+                double t = 0.0;
+                for (int i = 0; i < S; ++i) t += s->G[(size_t)i * M + a] * sg[i] * s->G[(size_t)i * M + b];
+                s->H[a * M + b] += t;
+                if (b != a) s->H[b * M + a] += t;
+            }
+            s->H[a * M + a] += sg[S + a];
+            double t = s->g[a] + bb[S + a];
+            for (int i = 0; i < S; ++i) t += s->G[(size_t)i * M + a] * tv[i];
+            s->du[a] = -t;
+        }
+        if (chol_solve(M, s->H, s->du) != 0) { status = ORACLE_FACTORIZATION_FAILED; break; }
+        memset(s->dx, 0, sizeof(double) * NX);
+        for (int k = 0; k < N; ++k)
+            for (int r = 0; r < NX; ++r) {
+                double t = s->c[k * NX + r];
+                for (int q = 0; q < NX; ++q) t += s->Ad[k * NX * NX + r * NX + q] * s->dx[k * NX + q];
+                for (int q = 0; q < NU; ++q) t += s->Bd[k * NX * NU + r * NU + q] * s->du[k * NU + q];
+                s->dx[(k + 1) * NX + r] = t;
+            }
+        for (int i = 0; i < S; ++i) dy[i] = s->dx[NX + i];
+        for (int a = 0; a < M; ++a) dy[S + a] = s->du[a];
+        /* fraction to the boundary: primal alpha_max, dual alpha_z */
+        const double tau = IP_TAU;
+        double amax = 1.0, az = 1.0, dbar = 0.0;
+        for (int i = 0; i < NY; ++i) {
+            const double y = YV(i);
+            if (yl[i] > -INFINITY) {
+                const double sl = y - yl[i];
+                if (dy[i] < 0.0) amax = fmin(amax, -tau * sl / dy[i]);
+                const double dz = mu_b / sl - zl[i] - zl[i] / sl * dy[i];
+                if (dz < 0.0) az = fmin(az, -tau * zl[i] / dz);
+            }
+            if (yu[i] < INFINITY) {
+                const double su = yu[i] - y;
+                if (dy[i] > 0.0) amax = fmin(amax, tau * su / dy[i]);
+                const double dz = mu_b / su - zu[i] + zu[i] / su * dy[i];
+                if (dz < 0.0) az = fmin(az, -tau * zu[i] / dz);
+            }
+            dbar += 2.0 * bb[i] * dy[i];  /* J-scale directional derivative of -2 mu sum log s */
+        }
+        /* l1-merit Armijo backtracking from alpha_max on J - 2 mu sum log s + nu |c|_1 */
+        double nu_new = 4.0 * lmax + 1.0;
+        if (nu_new > nu_pen) nu_pen = nu_new;
+        double J0 = 0.0, c1 = 0.0, dJ = 0.0;
+        for (int k = 0; k < N; ++k) {
+            double qe[ORACLE_MAX_NX];
+            for (int r = 0; r < NX; ++r) {
+                qe[r] = 2.0 * Q[r] * (s->F[k * NX + r] - traj[k * NX + r]);
+                J0 += 0.5 * qe[r] * (s->F[k * NX + r] - traj[k * NX + r]);
+                c1 += fabs(s->c[k * NX + r]);
+            }
+            for (int r = 0; r < NX; ++r) {
+                double ax = 0.0, bu = 0.0;
+                for (int q = 0; q < NX; ++q) ax += s->Ad[k * NX * NX + r * NX + q] * s->dx[k * NX + q];
+                for (int q = 0; q < NU; ++q) bu += s->Bd[k * NX * NU + r * NU + q] * s->du[k * NU + q];
+                dJ += qe[r] * (ax + bu);
+            }
+            for (int q = 0; q < NU; ++q) {
+                double um = (k == 0) ? u_prev[q] : s->U[(k - 1) * NU + q];
+                double dum = (k == 0) ? 0.0 : s->du[(k - 1) * NU + q];
+                double dif = s->U[k * NU + q] - um;
+                J0 += dif * R[q] * dif + s->U[k * NU + q] * Rm[q] * s->U[k * NU + q];
+                dJ += 2.0 * R[q] * dif * (s->du[k * NU + q] - dum) + 2.0 * Rm[q] * s->U[k * NU + q] * s->du[k * NU + q];
+            }
+        }
+        const double phi0 = J0 - 2.0 * mu_b * logsum + nu_pen * c1;
+        const double dphi = dJ + dbar - nu_pen * c1;
+        double alpha = amax;
+        int accepted = 0;
+        for (int ls = 0; ls < 30; ++ls) {
+            for (int i = 0; i < (N + 1) * NX; ++i) s->Xt[i] = s->X[i] + alpha * s->dx[i];
+            for (int i = 0; i < M; ++i) s->Ut[i] = s->U[i] + alpha * s->du[i];
+            double Jt, ct, lt = 0.0;
+            merit_eval(N, h, s->Xt, s->Ut, u_prev, traj, w, s->Ft, &Jt, &ct);
+            for (int i = 0; i < NY; ++i) {
+                const double y = (i < S) ? s->Xt[NX + i] : s->Ut[i - S];
+                if (yl[i] > -INFINITY) lt += log(y - yl[i]);
+                if (yu[i] < INFINITY) lt += log(yu[i] - y);
+            }
+            const double phit = Jt - 2.0 * mu_b * lt + nu_pen * ct;
+            const double noise = 1.0 + fabs(phi0);
+            if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) { accepted = 1; break; }
+            alpha *= 0.5;
+        }
+        if (!accepted) { status = ORACLE_LINESEARCH_FAILED; break; }
+        /* duals: z + alpha_z dz (dz at the old point), then the kappa_Sigma safeguard at the new point */
+        for (int i = 0; i < NY; ++i) {
+            const double y = YV(i);
+            if (yl[i] > -INFINITY) zl[i] += az * (mu_b / (y - yl[i]) - zl[i] - zl[i] / (y - yl[i]) * dy[i]);
+            if (yu[i] < INFINITY) zu[i] += az * (mu_b / (yu[i] - y) - zu[i] + zu[i] / (yu[i] - y) * dy[i]);
+        }
+        memcpy(s->X, s->Xt, sizeof(double) * (N + 1) * NX);
+        memcpy(s->U, s->Ut, sizeof(double) * M);
+        for (int i = 0; i < NY; ++i) {
+            const double y = YV(i);
+            if (yl[i] > -INFINITY) {
+                const double sl = y - yl[i];
+                zl[i] = fmax(fmin(zl[i], IP_KAPPA_SIGMA * mu_b / sl), mu_b / (IP_KAPPA_SIGMA * sl));
+            }
+            if (yu[i] < INFINITY) {
+                const double su = yu[i] - y;
+                zu[i] = fmax(fmin(zu[i], IP_KAPPA_SIGMA * mu_b / su), mu_b / (IP_KAPPA_SIGMA * su));
+            }
+        }
+        mu_b = mu_next;
+    }
+#undef YV
+    for (int k = 0; k < N; ++k) {
+        memcpy(V + k * ND, s->X + k * NX, sizeof(double) * NX);
+        memcpy(V + k * ND + NX, s->U + k * NU, sizeof(double) * NU);
+    }
+    memcpy(V + N * ND, s->X + N * NX, sizeof(double) * NX);
+    if (J_out) {
+        double J;
+        oracle_nlp_eval(t_model, N, h, V, u_prev, traj, w, &J, NULL);
+        *J_out = J;
+    }
+    free(yl); free(yu); free(zl); free(zu); free(sg); free(bb); free(zg); free(dy); free(tv);
+    *iters_out = it;
+    *kkt_out = kkt;
+    return status;
+}
+
 int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, const double* x0,
                        const double* u_prev, const double* traj, const double* weights,
                        int64_t w_stride, const double* u_lb, const double* u_ub, int max_iter,
                        double tol_grad, double tol_defect, double* V, int32_t* status,
                        int32_t* iters, double* kkt, double* Jout, int nthreads) {
+    return oracle_solve_batch_xb(model, is_linear, N, h, B, x0, u_prev, traj, weights, w_stride, u_lb, u_ub, NULL,
+                                 NULL, max_iter, tol_grad, tol_defect, V, status, iters, kkt, Jout, nthreads);
+}
+
+int oracle_solve_batch_xb(int model, int is_linear, int N, double h, int64_t B, const double* x0,
+                          const double* u_prev, const double* traj, const double* weights, int64_t w_stride,
+                          const double* u_lb, const double* u_ub, const double* x_lb, const double* x_ub,
+                          int max_iter, double tol_grad, double tol_defect, double* V, int32_t* status,
+                          int32_t* iters, double* kkt, double* Jout, int nthreads) {
     if (set_model(model) != 0 || N < 1 || B < 0) return -1;
+    int x_bounded = 0;
+    for (int r = 0; r < NX; ++r) x_bounded |= (x_lb && x_lb[r] > -1e19) || (x_ub && x_ub[r] < 1e19);
     const int NV = NX * (N + 1) + NU * N;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -647,9 +968,14 @@ int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, con
             } else {
                 g_lin = NULL;
             }
-            status[b] = solve_one(&s, h, x0 + b * NX, u_prev + b * NU, traj + b * (int64_t)N * NX,
-                                  weights + b * w_stride, u_lb, u_ub, max_iter, tol_grad, tol_defect,
-                                  V + b * NV, &it, &kk, &J);
+            if (x_bounded)
+                status[b] = solve_one_ip(&s, h, x0 + b * NX, u_prev + b * NU, traj + b * (int64_t)N * NX,
+                                         weights + b * w_stride, u_lb, u_ub, x_lb, x_ub, max_iter, tol_grad,
+                                         tol_defect, V + b * NV, &it, &kk, &J);
+            else
+                status[b] = solve_one(&s, h, x0 + b * NX, u_prev + b * NU, traj + b * (int64_t)N * NX,
+                                      weights + b * w_stride, u_lb, u_ub, max_iter, tol_grad, tol_defect,
+                                      V + b * NV, &it, &kk, &J);
             iters[b] = it;
             kkt[b] = kk;
             if (Jout) Jout[b] = J;

@@ -82,6 +82,15 @@ int oracle_solve_batch(int model, int is_linear, int N, double h, int64_t B, con
                        double tol_grad, double tol_defect, double* V, int32_t* status,
                        int32_t* iters, double* kkt, double* Jout, int nthreads);
 
+/* as oracle_solve_batch, plus state bounds x_lb/x_ub [nx] on x_1..x_N (ModelControl.cpp:37-50; NULL or
+ * |b| >= 1e19 = unbounded).  Any finite state bound selects the primal-dual interior-point variant
+ * (solve_one_ip), which then also handles the control bounds. */
+int oracle_solve_batch_xb(int model, int is_linear, int N, double h, int64_t B, const double* x0,
+                          const double* u_prev, const double* traj, const double* weights, int64_t w_stride,
+                          const double* u_lb, const double* u_ub, const double* x_lb, const double* x_ub,
+                          int max_iter, double tol_grad, double tol_defect, double* V, int32_t* status,
+                          int32_t* iters, double* kkt, double* Jout, int nthreads);
+
 /* counter-based synthetic cfg#2 instances: splitmix64(seed, index) */
 void oracle_synth_two_link(uint64_t seed, int64_t first_index, int64_t B, int N, double h,
                            double* x0, double* u_prev, double* traj);

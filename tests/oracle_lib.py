@@ -46,6 +46,12 @@ def lib():
             C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_double, _dp, _ip, _ip, _dp, _dp, C.c_int,
         ]
         L.oracle_solve_batch.restype = C.c_int
+        L.oracle_solve_batch_xb.argtypes = [
+            C.c_int, C.c_int, C.c_int, C.c_double, C.c_int64, _dp, _dp, _dp, _dp, C.c_int64,
+            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_double, C.c_double, _dp, _ip, _ip, _dp,
+            _dp, C.c_int,
+        ]
+        L.oracle_solve_batch_xb.restype = C.c_int
         L.oracle_synth_two_link.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int, C.c_double, _dp, _dp, _dp]
         L.oracle_synth_exo.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int, C.c_double, _dp, _dp, _dp]
         L.oracle_exo_jac.argtypes = [_dp, _dp, _dp, _dp, _dp]
@@ -155,7 +161,7 @@ def synth(seed, first, B, N, h, model=TWO_LINK):
 
 
 def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=50,
-                tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK):
+                tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK, x_lb=None, x_ub=None):
     NX, NU = DIMS[model]
     x0 = c64(x0).reshape(-1, NX)
     B = x0.shape[0]
@@ -166,9 +172,12 @@ def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, m
     st = np.zeros(B, np.int32); it = np.zeros(B, np.int32); kkt = np.zeros(B); J = np.zeros(B)
     lb = None if u_lb is None else c64(u_lb)
     ub = None if u_ub is None else c64(u_ub)
-    rc = lib().oracle_solve_batch(
+    xl = None if x_lb is None else c64(x_lb)
+    xu = None if x_ub is None else c64(x_ub)
+    ptr = lambda a: None if a is None else a.ctypes.data  # noqa: E731
+    rc = lib().oracle_solve_batch_xb(
         model, int(is_linear), N, h, B, x0.reshape(-1), c64(u_prev).reshape(-1), c64(traj).reshape(-1), weights.reshape(-1),
-        w_stride, None if lb is None else lb.ctypes.data, None if ub is None else ub.ctypes.data,
-        max_iter, tol_grad, tol_defect, V.reshape(-1), st, it, kkt, J, nthreads)
+        w_stride, ptr(lb), ptr(ub), ptr(xl), ptr(xu), max_iter, tol_grad, tol_defect, V.reshape(-1), st, it, kkt, J,
+        nthreads)
     assert rc == 0
     return dict(V=V, status=st, iters=it, kkt=kkt, J=J)

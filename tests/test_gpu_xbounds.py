@@ -1,0 +1,128 @@
+"""GPU: state bounds -- the interior-point variant of the 16-lane Riccati kernel
+(sqp_group.h XB; the same algorithm as oracle/mmpc_oracle.c solve_one_ip).
+
+* against the oracle on the same inputs: V* within 1e-9 relative where the iteration counts agree (>= 90 %),
+  1e-6 everywhere, identical statuses -- cfg#2-recipe instances with velocity bounds, with velocity + control
+  bounds, and position bounds (x_0 outside the box is infeasible: IPOPT would report infeasibility, both
+  implementations report a failure status for the same instances);
+* against the scipy golden vectors (tests/golden/xbounds_golden.json): V* within 1e-6, the same active bounds;
+* full size (cfg#2, B = 4096, velocity bounds): every instance converged, every state inside its box,
+  the device NLP evaluation confirms ||g||_inf <= 1e-10;
+* state bounds come from the model JSON (x_min/x_max, ModelControl.cpp:37-50) or mmpc_set_state_bounds.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import WEIGHTS_CFG, load_golden
+
+pytestmark = pytest.mark.gpu
+INF = np.inf
+
+
+def states(V, N, nx, nu):
+    return np.stack([V[:, k * (nx + nu):k * (nx + nu) + nx] for k in range(1, N + 1)], 1)
+
+
+def compare(g, o, tight=1e-9):
+    # the same instances converge; an infeasible instance (x_0 outside the box) fails in both, where the
+    # failure surfaces (max_iter / factorisation) depends on roundoff
+    assert np.array_equal(g["status"] == 0, o["status"] == 0), (np.bincount(g["status"]), np.bincount(o["status"]))
+    ok = g["status"] == 0
+    same = (g["iters"] == o["iters"]) & ok
+    assert same.sum() >= 0.9 * ok.sum(), (g["iters"], o["iters"])
+    rel = np.abs(g["V"] - o["V"]).max(axis=1) / np.abs(o["V"][ok]).max()
+    assert rel[same].max() < tight, rel[same].max()
+    assert rel[ok].max() < 1e-6
+
+
+CASES = {
+    "velocity": ([-INF, -INF, -1.5, -1.5], [INF, INF, 1.5, 1.5], None, None),
+    "velocity+u": ([-INF, -INF, -2.0, -2.0], [INF, INF, 2.0, 2.0], [-4.0, -4.0], [4.0, 4.0]),
+    "position": ([-0.6, -0.6, -3.0, -3.0], [0.6, 0.6, 3.0, 3.0], None, None),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_state_bounds_match_oracle(case, model_json, mmpc_mod, oracle):
+    xl, xu, ul, uu = (None if v is None else np.array(v) for v in CASES[case])
+    N, h, B = 30, 0.002, 128
+    s = mmpc_mod.Solver(model_json(N=N), max_iter=100)
+    s.set_state_bounds(xl, xu)
+    assert s.kkt_solver_for(B) == mmpc_mod.KKT_RICCATI_GROUP
+    x0, up, tr = oracle.synth(20250213, 0, B, N, h)
+    w = np.array(WEIGHTS_CFG)
+    g = s.solve_batch_host(x0, up, tr, w, u_lb=ul, u_ub=uu)
+    o = oracle.solve_batch(N, h, x0, up, tr, w, u_lb=ul, u_ub=uu, x_lb=xl, x_ub=xu, max_iter=100)
+    compare(g, o)
+    ok = g["status"] == 0
+    X = states(g["V"][ok], N, 4, 2)
+    assert (X >= xl - 1e-12).all() and (X <= xu + 1e-12).all()
+    if case == "position":
+        assert (~ok).sum() > 0  # x_0 outside the position box: infeasible instances fail in both
+    else:
+        assert ok.all()
+
+
+def test_state_bounds_match_scipy_golden(mmpc_mod, oracle, tmp_path):
+    gold = load_golden("xbounds_golden.json")
+    h = gold["h"]
+    for i, case in enumerate(gold["cases"]):
+        exo = case["model"] == "exo_arm"
+        nx, nu = (8, 4) if exo else (4, 2)
+        path = mmpc_mod.write_model_json(str(tmp_path / f"m{i}.json"), f"m{i}", nx, nu, int(h * 1e6), case["N"],
+                                         x_min=case["x_lb"], x_max=case["x_ub"],
+                                         model="exo_arm" if exo else "two_link_arm")
+        s = mmpc_mod.Solver(path, max_iter=200, kkt_solver=mmpc_mod.KKT_RICCATI_GROUP)
+        lb, ub = s.state_bounds()  # from the JSON (ModelParameters.cpp:66-69: +-10e30 -> +-inf)
+        assert np.array_equal(np.isfinite(lb), np.isfinite(case["x_lb"]))
+        ul, uu = np.array(case["u_lb"]), np.array(case["u_ub"])
+        g = s.solve_batch_host(np.array(case["x0"])[None], np.array(case["u_prev"])[None],
+                               np.array(case["traj"])[None], np.array(case["weights"]),
+                               u_lb=None if np.isinf(ul).all() else ul, u_ub=None if np.isinf(uu).all() else uu)
+        assert g["status"][0] == 0, (i, g["status"], g["iters"])
+        Vg = np.array(case["V"])
+        assert np.abs(g["V"][0] - Vg).max() / np.abs(Vg).max() < 1e-6, i
+
+
+def test_state_bounds_full_size(model_json, mmpc_mod):
+    N, B = 30, 4096
+    s = mmpc_mod.Solver(model_json(N=N, x_min=[-1e31, -1e31, -1.5, -1.5], x_max=[1e31, 1e31, 1.5, 1.5]),
+                        max_iter=100)
+    f = dict(dtype=torch.float64, device="cuda")
+    x0 = torch.empty((B, 4), **f); up = torch.empty((B, 2), **f); tr = torch.empty((B, N, 4), **f)
+    s.synth(20250213, 0, B, x0, up, tr)
+    w = torch.tensor(WEIGHTS_CFG, **f)
+    V = torch.zeros((B, s.NV), **f)
+    st = torch.zeros(B, dtype=torch.int32, device="cuda")
+    it = torch.zeros(B, dtype=torch.int32, device="cuda")
+    s.solve_batch(B, x0, up, tr, w, V, st, it, None)
+    J = torch.zeros(B, **f); gi = torch.zeros(B, **f)
+    s.nlp_eval(B, V, up, tr, w, J, gi)
+    torch.cuda.synchronize()
+    assert (st == 0).all(), torch.bincount(st.long())
+    assert gi.max().item() <= 1e-10
+    X = states(V.cpu().numpy(), N, 4, 2)
+    assert np.abs(X[:, :, 2:]).max() <= 1.5 + 1e-12
+    assert (np.abs(np.abs(X[:, :, 2:]) - 1.5) < 1e-6).sum() > 100  # many bounds active
+
+
+def test_state_bounds_api(model_json, mmpc_mod):
+    s = mmpc_mod.Solver(model_json(N=10))
+    lb, ub = s.state_bounds()
+    assert np.isinf(lb).all() and np.isinf(ub).all()
+    assert s.kkt_solver_for(64) == mmpc_mod.KKT_CONDENSED
+    s.set_state_bounds([-1.0] * 4, [1.0] * 4)
+    assert s.kkt_solver_for(64) == mmpc_mod.KKT_RICCATI_GROUP  # AUTO leaves the condensed solver
+    with pytest.raises(mmpc_mod.MmpcError):
+        s.set_state_bounds([1.0] * 4, [-1.0] * 4)
+    forced = mmpc_mod.Solver(model_json(N=10, name="f", x_min=[-1.0] * 4, x_max=[1.0] * 4),
+                             kkt_solver=mmpc_mod.KKT_CONDENSED)
+    x0 = np.zeros((1, 4)); up = np.zeros((1, 2)); tr = np.zeros((1, 10, 4))
+    with pytest.raises(mmpc_mod.MmpcError) as e:
+        forced.solve_batch_host(x0, up, tr, np.array(WEIGHTS_CFG))
+    assert e.value.code == -4
+    s.set_state_bounds(None, None)
+    assert s.kkt_solver_for(64) == mmpc_mod.KKT_CONDENSED

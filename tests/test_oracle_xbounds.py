@@ -1,0 +1,65 @@
+"""CPU: state bounds (x_k in [x_min, x_max] for k >= 1; ModelControl.cpp:37-50,146-157).
+
+The oracle's primal-dual interior-point variant (oracle/mmpc_oracle.c solve_one_ip) against the
+independent scipy SLSQP solves of tests/golden/xbounds_golden.json (single-shooting form, state bounds as
+inequality constraints, polished to a KKT point): V* within 1e-6 relative, J* within 1e-8 relative, the same
+active state bounds, every returned state inside its box.  Plus: the interior-point path reduces to the
+unbounded solution when the bounds are inactive, and control bounds alone still take the projected method.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return load_golden("xbounds_golden.json")
+
+
+def states(V, N, nx, nu):
+    return np.array([V[k * (nx + nu):k * (nx + nu) + nx] for k in range(1, N + 1)])
+
+
+def test_oracle_state_bounds_match_scipy(golden, oracle):
+    h = golden["h"]
+    for case in golden["cases"]:
+        model = oracle.EXO if case["model"] == "exo_arm" else oracle.TWO_LINK
+        nx, nu = oracle.DIMS[model]
+        N = case["N"]
+        r = oracle.solve_batch(N, h, np.array(case["x0"])[None], np.array(case["u_prev"])[None],
+                               np.array(case["traj"])[None], np.array(case["weights"]),
+                               u_lb=np.array(case["u_lb"]), u_ub=np.array(case["u_ub"]), x_lb=np.array(case["x_lb"]),
+                               x_ub=np.array(case["x_ub"]), max_iter=200, model=model)
+        assert r["status"][0] == 0, (case["index"], r["status"], r["iters"])
+        V, Vg = r["V"][0], np.array(case["V"])
+        assert np.abs(V - Vg).max() / np.abs(Vg).max() < 1e-6, (case["index"], np.abs(V - Vg).max())
+        assert abs(r["J"][0] - case["J"]) / case["J"] < 1e-8
+        X = states(V, N, nx, nu)
+        xl, xu = np.array(case["x_lb"]), np.array(case["x_ub"])
+        assert (X >= xl - 1e-12).all() and (X <= xu + 1e-12).all()
+        Xg = states(Vg, N, nx, nu)
+        act_g = (np.abs(Xg - xl) < 1e-9) | (np.abs(Xg - xu) < 1e-9)
+        act = (np.abs(X - xl) < 1e-6) | (np.abs(X - xu) < 1e-6)
+        assert act_g.sum() == case["n_active_x"] and (act == act_g).all()
+
+
+def test_inactive_state_bounds_reduce_to_unbounded(oracle):
+    N, h = 30, 0.002
+    x0, up, tr = oracle.synth(20250213, 0, 16, N, h)
+    w = np.array([10.0, 1.0, 5.0, 5.0, 5.0, 5.0, 0.01, 0.01])
+    a = oracle.solve_batch(N, h, x0, up, tr, w)
+    b = oracle.solve_batch(N, h, x0, up, tr, w, x_lb=np.full(4, -50.0), x_ub=np.full(4, 50.0), max_iter=100)
+    assert (a["status"] == 0).all() and (b["status"] == 0).all()
+    assert (b["iters"] > a["iters"]).all()  # the barrier path takes its own iterations ...
+    assert np.abs(a["V"] - b["V"]).max() / np.abs(a["V"]).max() < 1e-7  # ... to the same solution
+
+
+def test_infinite_state_bounds_keep_projected_method(oracle):
+    N, h = 30, 0.002
+    x0, up, tr = oracle.synth(20250213, 0, 8, N, h)
+    w = np.array([10.0, 1.0, 5.0, 5.0, 5.0, 5.0, 0.01, 0.01])
+    lb, ub = np.array([-2.0, -2.0]), np.array([2.0, 2.0])
+    a = oracle.solve_batch(N, h, x0, up, tr, w, u_lb=lb, u_ub=ub)
+    b = oracle.solve_batch(N, h, x0, up, tr, w, u_lb=lb, u_ub=ub, x_lb=np.full(4, -1e31), x_ub=np.full(4, 1e31))
+    assert np.array_equal(a["V"], b["V"]) and np.array_equal(a["iters"], b["iters"])
