@@ -394,9 +394,9 @@ int model_nq(int model_id) {
     return nq;
 }
 
-size_t workspace_bytes(const mmpc_model_info& mi, int nq, int64_t B) {
+size_t workspace_bytes(const mmpc_model_info& mi, int nq, int64_t B, bool xb = true) {
     const int64_t blocks = (B + 63) / 64;
-    return static_cast<size_t>(lane_ws_doubles(mi.num_x, mi.num_u, nq, mi.num_shooting_nodes)) * 64u *
+    return static_cast<size_t>(lane_ws_doubles(mi.num_x, mi.num_u, nq, mi.num_shooting_nodes, xb)) * 64u *
            static_cast<size_t>(blocks) * sizeof(double);
 }
 
@@ -425,9 +425,6 @@ int resolve_kkt_solver(const mmpc_handle* h, int64_t B) {
     const int s = resolve_kkt_solver_base(h, B);
     // state bounds (interior-point variant): the Riccati solvers only
     if (h->x_bounded && h->opts.kkt_solver == MMPC_KKT_AUTO && s == MMPC_KKT_CONDENSED) return MMPC_KKT_RICCATI_GROUP;
-    if (h->x_bounded && h->opts.kkt_solver == MMPC_KKT_AUTO && s == MMPC_KKT_RICCATI &&
-        group_lds_bytes(h->info, h->nq, false, true) <= kMaxGroupLds)
-        return MMPC_KKT_RICCATI_GROUP;  // until the lane kernel has the interior-point variant
     return s;
 }
 int resolve_kkt_solver_base(const mmpc_handle* h, int64_t B) {
@@ -488,8 +485,9 @@ int ensure_state_bounds_device(mmpc_handle* h, const double** lb, const double**
 }
 
 template <class Model, class FT>
-void launch_lane(bool bounded, dim3 grid, dim3 block, hipStream_t stream, const SolveParams& p, LaneWork lw) {
-    if (bounded) sqp_lane_kernel<Model, FT, true><<<grid, block, 0, stream>>>(p, lw);
+void launch_lane(bool bounded, bool xb, dim3 grid, dim3 block, hipStream_t stream, const SolveParams& p, LaneWork lw) {
+    if (xb) sqp_lane_kernel<Model, FT, false, true><<<grid, block, 0, stream>>>(p, lw);
+    else if (bounded) sqp_lane_kernel<Model, FT, true><<<grid, block, 0, stream>>>(p, lw);
     else sqp_lane_kernel<Model, FT, false><<<grid, block, 0, stream>>>(p, lw);
 }
 
@@ -585,8 +583,8 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         MMPC_HIP(hipGetLastError());
         return MMPC_OK;
     }
-    if (p.x_lb && solver != MMPC_KKT_RICCATI_GROUP)
-        return fail(MMPC_ERR_UNSUPPORTED, "state bounds need a Riccati solver (MMPC_KKT_RICCATI_GROUP)");
+    if (p.x_lb && solver == MMPC_KKT_CONDENSED)
+        return fail(MMPC_ERR_UNSUPPORTED, "state bounds need a Riccati solver (MMPC_KKT_RICCATI[_GROUP])");
     if (solver == MMPC_KKT_CONDENSED) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 is a Riccati-solver option");
 #if MMPC_BUILTIN_MODELS
@@ -614,8 +612,8 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         const bool f32 = h->opts.factor_fp32 != 0;
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
-            if (f32) launch_lane<M, float>(bounded, grid, block, stream, p, lw);
-            else launch_lane<M, double>(bounded, grid, block, stream, p, lw);
+            if (f32) launch_lane<M, float>(bounded, p.x_lb != nullptr, grid, block, stream, p, lw);
+            else launch_lane<M, double>(bounded, p.x_lb != nullptr, grid, block, stream, p, lw);
             return MMPC_OK;
         });
         if (rc) return rc;

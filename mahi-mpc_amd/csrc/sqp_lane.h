@@ -33,21 +33,24 @@ namespace mmpc {
 // per-lane pointer per (field, element) and spills).  Stage N holds x_N, d_N, dx_N; stages N+1.. hold
 // the linear-mode data (one stage for the built-in models); the stage(s) after it are per-lane scratch for
 // the Riccati step (W = P_xx A).  A field block longer than a stage simply runs on into the next stage.
-__host__ __device__ constexpr int lane_stage_stride(int nx, int nu) { return 5 * nx + 3 * nu + nu * (nx + nu + 1); }
+// xb: the interior-point variant's per-stage z_l, z_u, Sigma, b, z_u - z_l of (x_{k+1} | u_k) replace the hold field
+__host__ __device__ constexpr int lane_stage_stride(int nx, int nu, bool xb = false) {
+    return 5 * nx + 2 * nu + nu * (nx + nu + 1) + (xb ? 5 * (nx + nu) : nu);
+}
 // linear-mode block: h-free Jacobian blocks da/dq (na x nq), da/dz (na x na), da/du (na x nu), xdot*, x*, u*
 __host__ __device__ constexpr int lane_lin_doubles(int nx, int nu, int nq) {
     return (nx - nq) * (nq + (nx - nq) + nu) + 2 * nx + nu;
 }
-__host__ __device__ constexpr int lane_lin_stages(int nx, int nu, int nq) {
-    return (lane_lin_doubles(nx, nu, nq) + lane_stage_stride(nx, nu) - 1) / lane_stage_stride(nx, nu);
+__host__ __device__ constexpr int lane_lin_stages(int nx, int nu, int nq, bool xb = false) {
+    return (lane_lin_doubles(nx, nu, nq) + lane_stage_stride(nx, nu, xb) - 1) / lane_stage_stride(nx, nu, xb);
 }
-__host__ __device__ constexpr int lane_scratch_stages(int nx, int nu) {
-    return (nx * nx + lane_stage_stride(nx, nu) - 1) / lane_stage_stride(nx, nu);
+__host__ __device__ constexpr int lane_scratch_stages(int nx, int nu, bool xb = false) {
+    return (nx * nx + lane_stage_stride(nx, nu, xb) - 1) / lane_stage_stride(nx, nu, xb);
 }
-__host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int nq, int N) {
-    return (N + 1 + lane_lin_stages(nx, nu, nq) + lane_scratch_stages(nx, nu)) * lane_stage_stride(nx, nu);
+__host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int nq, int N, bool xb = false) {
+    return (N + 1 + lane_lin_stages(nx, nu, nq, xb) + lane_scratch_stages(nx, nu, xb)) * lane_stage_stride(nx, nu, xb);
 }
-template <int NX, int NU>
+template <int NX, int NU, bool XB = false>
 struct StageFields {
     static constexpr int NS = NX + NU;
     static constexpr int X = 0;             // x_k
@@ -59,8 +62,11 @@ struct StageFields {
     static constexpr int DU = DX + NX;      // du_k
     static constexpr int K = DU + NU;       // kff_k (nu, fp64) then K_k (nu x (nx+nu), factor type)
     static constexpr int HOLD = K + NU * (NS + 1);  // bounded solves: bound u_k is held at, NaN = free
-    static constexpr int SS = HOLD + NU;
-    static_assert(SS == lane_stage_stride(NX, NU), "layout");
+    // interior point (XB, no hold field): y = (x_{k+1} | u_k) duals, Sigma, b, z_u - z_l
+    static constexpr int NY = NX + NU;
+    static constexpr int ZL = HOLD, ZU = ZL + NY, SG = ZU + NY, BB = SG + NY, ZG = BB + NY;
+    static constexpr int SS = XB ? ZG + NY : HOLD + NU;
+    static_assert(SS == lane_stage_stride(NX, NU, XB), "layout");
 };
 
 struct LaneWork {
@@ -121,8 +127,10 @@ __device__ __forceinline__ double* stage_ptr(double* wsb, int64_t k, int SS, int
 // FT: arithmetic type of the Riccati factor/solve (double, or float for SURVEY.md 8d cfg#5: the backward
 // recursion, P in LDS, the gains K and the W scratch in fp32; model evaluations, defects, adjoint, gradient,
 // merit and iterates stay fp64, so every SQP iteration refines the fp32 step against fp64 residuals).
-template <class Model, class FT = double, bool BOUNDED = false>
+// XB: state bounds, the primal-dual interior-point variant (oracle solve_one_ip; see sqp_group.h)
+template <class Model, class FT = double, bool BOUNDED = false, bool XB = false>
 __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw) {
+    static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
     constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)
     static_assert(NQ >= 0 && NA >= NQ, "x = [q; z] with qdot = z[0:NQ]");
@@ -138,11 +146,12 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     const int N = p.N;
     const int NV = NX * (N + 1) + NU * N;
     const double h = p.h;
-    using SF = StageFields<NX, NU>;
+    using SF = StageFields<NX, NU, XB>;
+    constexpr int NY = NX + NU;
     constexpr int SS = SF::SS;
     const int lane = threadIdx.x;
-    double* __restrict__ const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)lane_ws_doubles(NX, NU, NQ, N) * 64);  // wave-uniform
-    const int kScratch = N + 1 + lane_lin_stages(NX, NU, NQ);  // first stage of the W = P_xx A scratch
+    double* __restrict__ const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)lane_ws_doubles(NX, NU, NQ, N, XB) * 64);  // wave-uniform
+    const int kScratch = N + 1 + lane_lin_stages(NX, NU, NQ, XB);  // first stage of the W = P_xx A scratch
 #define ST(k, f, e) wsb[((int64_t)(k) * SS + (f) + (e)) * 64 + lane]  // one-off accesses
 #define SK(dk, f, e) sk[((dk) * SS + (f) + (e)) * 64]                   // stage k + dk inside a stage loop
 
@@ -174,6 +183,20 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         for (int k = 0; k < N; ++k)
 #pragma unroll
             for (int r = 0; r < NX; ++r) ST(k, SF::R, r) = tr[k * NX + r];
+    }
+    double yl[XB ? NY : 1], yu[XB ? NY : 1];
+    double mub = kIpMu0;  // barrier parameter (f = J/2 scale)
+    if constexpr (XB) {  // y pushed into the interior, z = 1 on finite bounds (oracle solve_one_ip)
+        load_ip_bounds<NX, NU>(p, yl, yu);
+        for (int k = 0; k < N; ++k) {
+#pragma unroll
+            for (int j = 0; j < NY; ++j) {
+                double& y = j < NX ? ST(k + 1, SF::X, j) : ST(k, SF::U, j - NX);
+                y = ip_push(y, yl[j], yu[j]);
+                ST(k, SF::ZL, j) = yl[j] > -INFINITY ? 1.0 : 0.0;
+                ST(k, SF::ZU, j) = yu[j] < INFINITY ? 1.0 : 0.0;
+            }
+        }
     }
     // linear mode: acceleration Jacobians and xdot at (state, control) = (x_0, u_prev), ModelControl.cpp:125-135
     const bool lin = p.is_linear != 0;
@@ -254,6 +277,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     for (it = 0; it <= p.max_iter; ++it) {
         // ---- (1) forward: F, defects, d_{k+1} = A_k d_k + c_k, merit value ----
         double J0 = 0.0, c1 = 0.0, cmax = 0.0;
+        double lsum = 0.0, cmpl0 = 0.0, cmplmu = 0.0;  // interior point: sum log s, max |s z|, max |s z - mu|
         bool nonfinite = false;
         {
             // software pipeline: the model inputs of stage k+1 are loaded during stage k (one wave per SIMD
@@ -307,12 +331,25 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     J0 = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], J0));
                     um[c] = u[c];
                 }
+                if constexpr (XB) {  // barrier pieces of (x_{k+1} | u_k); xk now holds x_{k+1}
+#pragma unroll
+                    for (int j = 0; j < NY; ++j) {
+                        double sg, bb, zg;
+                        ip_terms(j < NX ? xk[j] : u[j - NX], yl[j], yu[j], SK(0, SF::ZL, j), SK(0, SF::ZU, j), mub, sg,
+                                 bb, zg, cmpl0, cmplmu, lsum);
+                        SK(0, SF::SG, j) = sg;
+                        SK(0, SF::BB, j) = bb;
+                        SK(0, SF::ZG, j) = zg;
+                    }
+                }
             }
+            nonfinite |= !isfinite(lsum);
         }
 
         MMPC_PHASE(1);
         // (2)+(3) run once, or (bounded) again after holding controls whose step crosses a bound
         double gmax = 0.0, lmax = 0.0, dJ = 0.0;
+        double mub_next = mub, amax = 1.0, az = 1.0, dbar = 0.0;  // interior point (XB)
         bool fact_ok = true, done = false;
         const double beps = BOUNDED ? fmin(kBoundEps, pg_prev) : 0.0;
         // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
@@ -339,6 +376,11 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     const double eb = ST(N, SF::X, r) - ST(N - 1, SF::R, r);  // x_N - r_{N-1}
                     pv[r] = Q[r] * eb;
                     lam[r] = Q[r] * (ST(N, SF::D, r) + eb);  // lam_N = Q e_{N-1}
+                    if constexpr (XB) {  // barrier at x_N
+                        PS(r, r) += (FT)ST(N - 1, SF::SG, r);
+                        pv[r] += ST(N - 1, SF::BB, r);
+                        lam[r] += ST(N - 1, SF::ZG, r);
+                    }
                     lmax = fmax(lmax, fabs(lam[r]));
                 }
                 // software pipeline as in (1): x_{k-1}, u_{k-1} (model inputs of the next step) are loaded during
@@ -389,6 +431,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         for (int s = 0; s < NA; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
                         g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
                         if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
+                        if (XB) g += SK(0, SF::ZG, NX + c);  // reduced Lagrangian gradient
                         if (!BOUNDED) {
                             gmax = fmax(gmax, fabs(2.0 * g));
                         } else {  // projected gradient; hold rule (pass 0) or the holds of the previous solve
@@ -412,6 +455,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
 #pragma unroll
                         for (int r = 0; r < NX; ++r) {
                             lam[r] = fma(Q[r], dk[r] + x[r] - rkm[r], ln[r]);
+                            if (XB) lam[r] += SK(-1, SF::ZG, r);
                             lmax = fmax(lmax, fabs(lam[r]));
                         }
                     }
@@ -457,9 +501,11 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                             for (int s = 0; s < NA; ++s)
                                 t = fma(fu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), fu[s * NU + b], t));
                             if (a == b) t += (FT)(R[a] + Rm[a]);
+                            if (XB && a == b) t += (FT)SK(0, SF::SG, NX + a);
                             Hww[a][b] = t;
                         }
                         double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
+                        if (XB) t += SK(0, SF::BB, NX + a);
 #pragma unroll
                         for (int s = 0; s < NA; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
 #pragma unroll
@@ -528,7 +574,10 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         double t[NX];
                         at_mul<NQ, NA, double>(h, hFq, hFqd, mv, t);
 #pragma unroll
-                        for (int q = 0; q < NX; ++q) pn[q] = fma(Q[q], x[q] - rkm[q], t[q]);
+                        for (int q = 0; q < NX; ++q) {
+                            pn[q] = fma(Q[q], x[q] - rkm[q], t[q]);
+                            if (XB) pn[q] += SK(-1, SF::BB, q);
+                        }
 #pragma unroll
                         for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
                     }
@@ -603,7 +652,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         at_mul<NQ, NA, FT>(hf, fq, fqd, wcol, col);
 #pragma unroll
                         for (int a = 0; a <= b; ++a) {
-                            FT v = col[a] + (FT)((a == b) ? Q[a] : 0.0);
+                            FT v = col[a] + (FT)((a == b) ? Q[a] + (XB ? SK(-1, SF::SG, a) : 0.0) : 0.0);
 #pragma unroll
                             for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
                             PS(a, b) = v;
@@ -629,6 +678,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             MMPC_PHASE(2);
             if (pass == 0) {
                 kkt = fmax(gmax, cmax);
+                if (XB) kkt = fmax(kkt, 2.0 * cmpl0);  // J-scale complementarity
                 if (trc) {
                     trc[0] = gmax;
                     trc[1] = cmax;
@@ -641,7 +691,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     done = true;
                     break;
                 }
-                if (gmax <= p.tol_grad && cmax <= p.tol_defect) {
+                if (gmax <= p.tol_grad && cmax <= p.tol_defect && (!XB || 2.0 * cmpl0 <= kIpTolCompl)) {
                     status = ST_CONVERGED;
                     done = true;
                     break;
@@ -652,6 +702,9 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     break;
                 }
                 if (BOUNDED) pg_prev = gmax;
+                // barrier update for the next iteration (IPOPT monotone rule, lagged; oracle solve_one_ip)
+                if (XB && fmax(fmax(0.5 * gmax, cmax), cmplmu) <= kIpKappaEps * mub)
+                    mub_next = fmax(kIpTolCompl / 20.0, fmin(kIpKappaMu * mub, pow(mub, kIpThetaMu)));
             }
             if (!fact_ok) {
                 status = ST_FACT_FAILED;
@@ -661,6 +714,9 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
 
             // ---- (3) forward: step (dx, du) and the directional derivative of J ----
             dJ = 0.0;
+            amax = 1.0;
+            az = 1.0;
+            dbar = 0.0;
             {
                 double dx[NX], dup[NU], um[NU];
 #pragma unroll
@@ -742,6 +798,13 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         um[c] = u[c];
                         dup[c] = du[c];
                     }
+                    if constexpr (XB) {  // fraction to the boundary of (x_{k+1} | u_k), barrier directional derivative
+#pragma unroll
+                        for (int j = 0; j < NY; ++j)
+                            ip_step_limits(j < NX ? xpf[j] : u[j - NX], j < NX ? dx[j] : du[j - NX], yl[j], yu[j],
+                                           SK(0, SF::ZL, j), SK(0, SF::ZU, j), mub, kIpTau, SK(0, SF::BB, j), amax,
+                                           az, dbar);
+                    }
                 }
             }
 
@@ -751,13 +814,13 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         if (done) break;
         // ---- (4) l1-merit Armijo line search (noise-aware, as sqp_wave.h) ----
         mu = fmax(mu, 4.0 * lmax + 1.0);
-        const double phi0 = fma(mu, c1, J0);
-        const double dphi = dJ - mu * c1;
-        double alpha = 1.0;
+        const double phi0 = XB ? fma(mu, c1, fma(-2.0 * mub, lsum, J0)) : fma(mu, c1, J0);
+        const double dphi = XB ? dJ + dbar - mu * c1 : dJ - mu * c1;
+        double alpha = XB ? amax : 1.0;
         bool accepted = false;
         #pragma unroll 1
         for (int ls = 0; ls < 30; ++ls) {
-            double Jt = 0.0, ct = 0.0, xk[NX], umt[NU], upf[NU], dupf[NU];
+            double Jt = 0.0, ct = 0.0, lt = 0.0, xk[NX], umt[NU], upf[NU], dupf[NU];
 #pragma unroll
             for (int r = 0; r < NX; ++r) xk[r] = ST(0, SF::X, r);  // dx_0 = 0
 #pragma unroll
@@ -800,8 +863,12 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     Jt = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], Jt));
                     umt[c] = u[c];
                 }
+                if constexpr (XB) {
+#pragma unroll
+                    for (int j = 0; j < NY; ++j) lt += ip_log_slacks(j < NX ? xn[j] : u[j - NX], yl[j], yu[j]);
+                }
             }
-            const double phit = fma(mu, ct, Jt);
+            const double phit = XB ? fma(mu, ct, fma(-2.0 * mub, lt, Jt)) : fma(mu, ct, Jt);
             const double noise = 1.0 + fabs(phi0);
             if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) {
                 accepted = true;
@@ -811,26 +878,45 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         }
         MMPC_PHASE(5);
         if (trc) {
-            trc[4] = dJ;
+            trc[4] = XB ? amax : dJ;
             trc[5] = alpha;
-            trc[6] = mu;
+            trc[6] = XB ? mub : mu;
+            if (XB) trc[3] = cmpl0;
         }
         if (!accepted) {
             status = ST_LS_FAILED;
             break;
         }
-        #pragma unroll 1
-        for (int k = 0; k <= N; ++k) {
+        if constexpr (XB) {  // y and the duals of stage k's (x_{k+1} | u_k), as oracle solve_one_ip
+            #pragma unroll 1
+            for (int k = 0; k < N; ++k) {
                 double* const sk = stage_ptr(wsb, k, SS, lane);
-            if (k > 0) {
 #pragma unroll
-                for (int r = 0; r < NX; ++r) SK(0, SF::X, r) = fma(alpha, SK(0, SF::DX, r), SK(0, SF::X, r));
+                for (int j = 0; j < NY; ++j) {
+                    double& y = j < NX ? SK(1, SF::X, j) : SK(0, SF::U, j - NX);
+                    const double dy = j < NX ? SK(1, SF::DX, j) : SK(0, SF::DU, j - NX);
+                    double zl = SK(0, SF::ZL, j), zu = SK(0, SF::ZU, j), yn;
+                    ip_update(y, dy, yl[j], yu[j], zl, zu, mub, alpha, az, yn);
+                    y = yn;
+                    SK(0, SF::ZL, j) = zl;
+                    SK(0, SF::ZU, j) = zu;
+                }
             }
-            if (k < N) {
+            mub = mub_next;
+        } else {
+            #pragma unroll 1
+            for (int k = 0; k <= N; ++k) {
+                double* const sk = stage_ptr(wsb, k, SS, lane);
+                if (k > 0) {
 #pragma unroll
-                for (int c = 0; c < NU; ++c) {
-                    const double un = fma(alpha, SK(0, SF::DU, c), SK(0, SF::U, c));
-                    SK(0, SF::U, c) = BOUNDED ? proj(un, lbv[c], ubv[c]) : un;
+                    for (int r = 0; r < NX; ++r) SK(0, SF::X, r) = fma(alpha, SK(0, SF::DX, r), SK(0, SF::X, r));
+                }
+                if (k < N) {
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {
+                        const double un = fma(alpha, SK(0, SF::DU, c), SK(0, SF::U, c));
+                        SK(0, SF::U, c) = BOUNDED ? proj(un, lbv[c], ubv[c]) : un;
+                    }
                 }
             }
         }

@@ -45,13 +45,15 @@ CASES = {
 }
 
 
+@pytest.mark.parametrize("solver", ["group", "lane"])
 @pytest.mark.parametrize("case", list(CASES))
-def test_state_bounds_match_oracle(case, model_json, mmpc_mod, oracle):
+def test_state_bounds_match_oracle(case, solver, model_json, mmpc_mod, oracle):
     xl, xu, ul, uu = (None if v is None else np.array(v) for v in CASES[case])
     N, h, B = 30, 0.002, 128
-    s = mmpc_mod.Solver(model_json(N=N), max_iter=100)
+    ks = mmpc_mod.KKT_RICCATI_GROUP if solver == "group" else mmpc_mod.KKT_RICCATI
+    s = mmpc_mod.Solver(model_json(N=N), max_iter=100, kkt_solver=ks)
     s.set_state_bounds(xl, xu)
-    assert s.kkt_solver_for(B) == mmpc_mod.KKT_RICCATI_GROUP
+    assert s.kkt_solver_for(B) == ks
     x0, up, tr = oracle.synth(20250213, 0, B, N, h)
     w = np.array(WEIGHTS_CFG)
     g = s.solve_batch_host(x0, up, tr, w, u_lb=ul, u_ub=uu)
@@ -66,8 +68,10 @@ def test_state_bounds_match_oracle(case, model_json, mmpc_mod, oracle):
         assert ok.all()
 
 
-def test_state_bounds_match_scipy_golden(mmpc_mod, oracle, tmp_path):
+@pytest.mark.parametrize("solver", ["group", "lane"])
+def test_state_bounds_match_scipy_golden(solver, mmpc_mod, oracle, tmp_path):
     gold = load_golden("xbounds_golden.json")
+    ks = mmpc_mod.KKT_RICCATI_GROUP if solver == "group" else mmpc_mod.KKT_RICCATI
     h = gold["h"]
     for i, case in enumerate(gold["cases"]):
         exo = case["model"] == "exo_arm"
@@ -75,7 +79,7 @@ def test_state_bounds_match_scipy_golden(mmpc_mod, oracle, tmp_path):
         path = mmpc_mod.write_model_json(str(tmp_path / f"m{i}.json"), f"m{i}", nx, nu, int(h * 1e6), case["N"],
                                          x_min=case["x_lb"], x_max=case["x_ub"],
                                          model="exo_arm" if exo else "two_link_arm")
-        s = mmpc_mod.Solver(path, max_iter=200, kkt_solver=mmpc_mod.KKT_RICCATI_GROUP)
+        s = mmpc_mod.Solver(path, max_iter=200, kkt_solver=ks)
         lb, ub = s.state_bounds()  # from the JSON (ModelParameters.cpp:66-69: +-10e30 -> +-inf)
         assert np.array_equal(np.isfinite(lb), np.isfinite(case["x_lb"]))
         ul, uu = np.array(case["u_lb"]), np.array(case["u_ub"])
@@ -107,6 +111,27 @@ def test_state_bounds_full_size(model_json, mmpc_mod):
     X = states(V.cpu().numpy(), N, 4, 2)
     assert np.abs(X[:, :, 2:]).max() <= 1.5 + 1e-12
     assert (np.abs(np.abs(X[:, :, 2:]) - 1.5) < 1e-6).sum() > 100  # many bounds active
+
+
+def test_exo_state_bounds_lane(mmpc_mod, oracle, tmp_path):
+    """Exo, N = 50 (cfg#3 shape): the group kernel's LDS cannot hold the interior-point data, AUTO runs the lane
+    kernel's interior-point variant; joint-velocity bounds +-0.3 rad/s."""
+    N, h, B = 50, 0.002, 64
+    xl = np.array([-INF] * 4 + [-0.3] * 4)
+    xu = np.array([INF] * 4 + [0.3] * 4)
+    path = mmpc_mod.write_model_json(str(tmp_path / "exo.json"), "exo", 8, 4, 2000, N, model="exo_arm",
+                                     x_min=[-1e31] * 4 + [-0.3] * 4, x_max=[1e31] * 4 + [0.3] * 4)
+    s = mmpc_mod.Solver(path, max_iter=100)
+    assert s.kkt_solver_for(B) == mmpc_mod.KKT_RICCATI
+    x0, up, tr = oracle.synth(20250213, 0, B, N, h, model=oracle.EXO)
+    x0[:, 4:] = np.clip(x0[:, 4:], -0.25, 0.25)
+    w = np.array([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4)
+    g = s.solve_batch_host(x0, up, tr, w)
+    o = oracle.solve_batch(N, h, x0, up, tr, w, x_lb=xl, x_ub=xu, max_iter=100, model=oracle.EXO)
+    compare(g, o)
+    assert (g["status"] == 0).all()
+    X = states(g["V"], N, 8, 4)
+    assert np.abs(X[:, :, 4:]).max() <= 0.3 + 1e-12
 
 
 def test_state_bounds_api(model_json, mmpc_mod):
