@@ -145,3 +145,25 @@ def test_closed_loop_example_on_generated_model(tmp_path):
     assert a.shape == b.shape and a.shape[0] == 50
     assert (a[:, 7] == 0).all()
     np.testing.assert_allclose(a[:, :7], b[:, :7], rtol=1e-8, atol=1e-9)
+
+
+@pytest.mark.parametrize("kkt", ["group", "riccati"])
+def test_generated_model_state_bounds(kkt, mmpc_mod, oracle):
+    """State bounds on a generated model (interior-point variant compiled into <name>.so): cart-pole with the
+    cart position in [-0.2, 0.2] m and the pole rate in [-1, 1] rad/s, against the oracle on the same dynamics."""
+    ks = mmpc_mod.KKT_RICCATI_GROUP if kkt == "group" else mmpc_mod.KKT_RICCATI
+    s = solver(mmpc_mod, "cart_pole", kkt_solver=ks, max_iter=100)
+    mid = oracle.use_user_model("cart_pole")
+    xl, xu = np.array([-0.2, -np.inf, -np.inf, -1.0]), np.array([0.2, np.inf, np.inf, 1.0])
+    s.set_state_bounds(xl, xu)
+    x0, up, tr = instances(s.nx, s.nu, 64, s.N, s.h, seed=5)
+    x0[:, 0] = np.clip(x0[:, 0], -0.15, 0.15)
+    x0[:, 3] = np.clip(x0[:, 3], -0.9, 0.9)
+    tr *= 3.0
+    w = weights(s.nx, s.nu)
+    g = s.solve_batch_host(x0, up, tr, w)
+    o = oracle.solve_batch(s.N, s.h, x0, up, tr, w, model=mid, x_lb=xl, x_ub=xu, max_iter=100)
+    compare(g, o)
+    X = np.stack([g["V"][:, k * 5:k * 5 + 4] for k in range(1, s.N + 1)], 1)
+    assert (X >= xl - 1e-12).all() and (X <= xu + 1e-12).all()
+    assert (np.abs(np.abs(X[:, :, 0]) - 0.2) < 1e-6).any()  # the position bound is active somewhere
