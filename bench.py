@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--no-gather", action="store_true", help="N > 1: skip gathering the results to rank 0")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--init", choices=["as_given", "hold_x0"], default="as_given",
+                    help="mmpc_opts.init_states: the reference's cold start (V = 0) or x_1..x_N = x_0 (DESIGN 3d)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch per config (tools/pmc.sh + tools/pmc_summary.py)")
     return ap.parse_args()
@@ -112,7 +114,8 @@ def main():
     path = mmpc.write_model_json(os.path.join(tmpdir, f"{cfg['model']}.json"), cfg["model"], nx, nu, h_us, N,
                                  model=cfg["model"])
     ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt]
-    solver = mmpc.Solver(path, device=local, kkt_solver=ksolver)
+    solver = mmpc.Solver(path, device=local, kkt_solver=ksolver,
+                         init_states=mmpc.INIT_HOLD_X0 if args.init == "hold_x0" else mmpc.INIT_AS_GIVEN)
     solver.reserve_workspace(B)
     ksolver = solver.kkt_solver_for(B)   # the AUTO choice, resolved by the library
     riccati = ksolver in (2, 3)
@@ -215,6 +218,8 @@ def main():
         "config": {"workload": cfg["workload"], "batch_per_gpu": B, "global_batch": B * world,
                    "horizon": N, "kkt_solver": {1: "condensed (wave per instance)", 2: "riccati (lane per instance)",
                                                 3: "riccati (16 lanes per instance)"}[ksolver],
+                   "init_states": "V as given (reference cold start V = 0)" if args.init == "as_given"
+                   else "x_1..x_N = x_0 (MMPC_INIT_HOLD_X0)",
                    "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) to rank 0 by "
                                    "RCCL all_gather_into_tensor, overlapped with the next solve"
                                    if gather else f"batch-shard x{world} (no collective on the solve path)")},

@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MMPC_ABI_VERSION 2
+#define MMPC_ABI_VERSION 3
 
 typedef struct mmpc_handle mmpc_handle;
 
@@ -106,6 +106,14 @@ enum mmpc_kkt_solver {
                                   serial Riccati sweeps from LDS (stage data of 4 instances <= 160 KB LDS) */
 };
 
+/* how a solve starts from V_inout (the converged KKT point does not depend on it) */
+enum mmpc_init_states {
+    MMPC_INIT_AS_GIVEN = 0, /* the reference: V as given (first call zeros, ModelControl.cpp:29-50; later the
+                               previous solution, :160-161), x_0 pinned to the measured state */
+    MMPC_INIT_HOLD_X0 = 1   /* x_1..x_N start at the measured state x_0 (controls as given): a consistent-ish
+                               state trajectory for cold starts, fewer SQP iterations */
+};
+
 typedef struct mmpc_opts {
     int32_t max_iter;   /* SQP iteration cap (reference IPOPT: 200, ModelControl.cpp:55). default 50 */
     int32_t device;     /* HIP device ordinal; -1 = the calling thread's current device. default -1 */
@@ -114,6 +122,7 @@ typedef struct mmpc_opts {
     int32_t kkt_solver; /* enum mmpc_kkt_solver. default MMPC_KKT_AUTO */
     int32_t factor_fp32; /* 1: Riccati factor/solve in fp32, residuals/merit/iterates in fp64 (SURVEY 8d
                             cfg#5; each SQP iteration refines the fp32 step). Riccati solver only. default 0 */
+    int32_t init_states; /* enum mmpc_init_states. default MMPC_INIT_AS_GIVEN */
 } mmpc_opts;
 
 typedef struct mmpc_model_info {

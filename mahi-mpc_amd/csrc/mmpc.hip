@@ -199,6 +199,8 @@ int validate_opts(const mmpc_opts* o) {
     if (o->kkt_solver < MMPC_KKT_AUTO || o->kkt_solver > MMPC_KKT_RICCATI_GROUP)
         return fail(MMPC_ERR_INVALID_ARG, "unknown kkt_solver");
     if (o->factor_fp32 != 0 && o->factor_fp32 != 1) return fail(MMPC_ERR_INVALID_ARG, "factor_fp32 must be 0 or 1");
+    if (o->init_states != MMPC_INIT_AS_GIVEN && o->init_states != MMPC_INIT_HOLD_X0)
+        return fail(MMPC_ERR_INVALID_ARG, "unknown init_states");
     return MMPC_OK;
 }
 
@@ -546,6 +548,7 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.iters = iters;
     p.kkt = kkt;
     p.trace = trace;
+    p.init_hold = h->opts.init_states == MMPC_INIT_HOLD_X0;
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
     // points pass NULL for bounds that are all infinite
     const bool bounded = u_lb || u_ub;
@@ -656,6 +659,7 @@ void mmpc_default_opts(mmpc_opts* o) {
     o->tol_defect = 1e-10;
     o->kkt_solver = MMPC_KKT_AUTO;
     o->factor_fp32 = 0;
+    o->init_states = MMPC_INIT_AS_GIVEN;
 }
 
 int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_handle** out) {

@@ -164,7 +164,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         const double* Vin = p.V + ii * (int64_t)NV;
         for (int k = gl; k <= N; k += G) {
 #pragma unroll
-            for (int r = 0; r < NX; ++r) sX[k * NX + r] = (k == 0) ? p.x0[ii * NX + r] : Vin[k * ND + r];
+            for (int r = 0; r < NX; ++r) sX[k * NX + r] = (k == 0 || p.init_hold) ? p.x0[ii * NX + r] : Vin[k * ND + r];
             if (k < N) {
 #pragma unroll
                 for (int c = 0; c < NU; ++c)

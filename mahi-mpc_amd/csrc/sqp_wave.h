@@ -53,6 +53,7 @@ struct SolveParams {
     int32_t* iters;
     double* kkt;
     double* trace;  // debug: [B][max_iter+1][8] per-iteration diagnostics, or nullptr
+    int init_hold;  // mmpc_opts.init_states == MMPC_INIT_HOLD_X0: x_1..x_N start at x_0 (controls as given)
 };
 
 enum {
@@ -319,11 +320,12 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
     for (int i = lane; i < NV; i += 64) {
         const int k = i / ND, r = i - k * ND;
         const double v = Vin[i];
+        const double xv = (p.init_hold && r < NX) ? p.x0[inst * NX + r] : v;  // state entries only
         if (k < N) {
-            if (r < NX) sX[k * NX + r] = v;
+            if (r < NX) sX[k * NX + r] = xv;
             else sU[k * NU + r - NX] = v;
         } else {
-            sX[N * NX + r] = v;
+            sX[N * NX + r] = xv;
         }
     }
     // stages >= N are structurally zero in the static-NMAX loops below

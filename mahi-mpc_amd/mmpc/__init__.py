@@ -40,6 +40,7 @@ class MmpcError(RuntimeError):
 
 
 KKT_AUTO, KKT_CONDENSED, KKT_RICCATI, KKT_RICCATI_GROUP = 0, 1, 2, 3
+INIT_AS_GIVEN, INIT_HOLD_X0 = 0, 1
 MODEL_TWO_LINK_ARM, MODEL_EXO_ARM, MODEL_USER = 0, 1, 2
 USER_LIB_DIR = os.path.join(ROOT, "lib", "user")
 BUILTIN_MODELS = ("two_link_arm", "double_pendulum", "exo_arm", "exo")  # "mmpc_model" names libmmpc.so serves   # models generated from SX by ModelGenerator (make -C host user)
@@ -47,7 +48,8 @@ BUILTIN_MODELS = ("two_link_arm", "double_pendulum", "exo_arm", "exo")  # "mmpc_
 
 class Opts(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("device", C.c_int32), ("tol_grad", C.c_double),
-                ("tol_defect", C.c_double), ("kkt_solver", C.c_int32), ("factor_fp32", C.c_int32)]
+                ("tol_defect", C.c_double), ("kkt_solver", C.c_int32), ("factor_fp32", C.c_int32),
+                ("init_states", C.c_int32)]
 
 
 class ModelInfo(C.Structure):
@@ -192,7 +194,7 @@ class Solver:
     """One loaded model (the reference's ModelControl without the thread/bookkeeping)."""
 
     def __init__(self, model_json=None, json_text=None, max_iter=None, tol_grad=None, tol_defect=None,
-                 device=None, kkt_solver=None, factor_fp32=None, library=None):
+                 device=None, kkt_solver=None, factor_fp32=None, library=None, init_states=None):
         self._L = L = lib(library or (model_library(model_json) if model_json is not None else None))
         o = Opts()
         L.mmpc_default_opts(C.byref(o))
@@ -200,6 +202,8 @@ class Solver:
             o.kkt_solver = kkt_solver
         if factor_fp32 is not None:
             o.factor_fp32 = int(factor_fp32)
+        if init_states is not None:
+            o.init_states = int(init_states)
         if max_iter is not None:
             o.max_iter = max_iter
         if tol_grad is not None:

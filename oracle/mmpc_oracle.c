@@ -36,6 +36,9 @@ static _Thread_local int t_model = ORACLE_MODEL_TWO_LINK_ARM, t_nx = 4, t_nu = 2
 #define ND (t_nx + t_nu)
 /* dynamics registered by oracle_set_user_model (process-wide; models generated from SX expressions) */
 static oracle_user_jac_fn g_user_jac = NULL;
+/* mmpc_opts.init_states (process-wide): 1 = x_1..x_N start at x_0 */
+static int g_init_hold = 0;
+void oracle_set_init_states(int mode) { g_init_hold = mode == 1; }
 static int g_user_nx = 0, g_user_nu = 0;
 static int set_model(int model) {
     if (model == ORACLE_MODEL_TWO_LINK_ARM) { t_model = model; t_nx = 4; t_nu = 2; return 0; }
@@ -396,6 +399,8 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
     }
     memcpy(s->X + N * NX, V + N * ND, sizeof(double) * NX);
     memcpy(s->X, x0, sizeof(double) * NX);
+    if (g_init_hold)  /* MMPC_INIT_HOLD_X0: the state trajectory starts at the measured state */
+        for (int k = 1; k <= N; ++k) memcpy(s->X + k * NX, x0, sizeof(double) * NX);
     /* box constraints on u (ModelControl.cpp:37-50,146-157; |b| >= 1e19 is unbounded, as IPOPT): projected
      * Gauss-Newton SQP -- the iterate starts projected, controls at a bound whose gradient points outward
      * (epsilon-active set, Bertsekas 1982) are held in the QP, trial points are projected onto the box and the
@@ -689,6 +694,8 @@ static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_pre
     }
     memcpy(s->X + N * NX, V + N * ND, sizeof(double) * NX);
     memcpy(s->X, x0, sizeof(double) * NX);
+    if (g_init_hold)  /* MMPC_INIT_HOLD_X0: the state trajectory starts at the measured state */
+        for (int k = 1; k <= N; ++k) memcpy(s->X + k * NX, x0, sizeof(double) * NX);
     for (int i = 0; i < NY; ++i) {
         double* p = (i < S) ? &s->X[NX + i] : &s->U[i - S];
         *p = ip_push(*p, yl[i], yu[i]);

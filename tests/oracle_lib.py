@@ -161,7 +161,18 @@ def synth(seed, first, B, N, h, model=TWO_LINK):
 
 
 def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=50,
-                tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK, x_lb=None, x_ub=None):
+                tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK, x_lb=None, x_ub=None,
+                init_states=0):
+    lib().oracle_set_init_states(int(init_states))
+    try:
+        return _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_grad, tol_defect, nthreads,
+                            is_linear, model, x_lb, x_ub)
+    finally:
+        lib().oracle_set_init_states(0)
+
+
+def _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_grad, tol_defect, nthreads,
+                 is_linear, model, x_lb, x_ub):
     NX, NU = DIMS[model]
     x0 = c64(x0).reshape(-1, NX)
     B = x0.shape[0]

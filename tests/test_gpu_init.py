@@ -1,0 +1,55 @@
+"""GPU: mmpc_opts.init_states = MMPC_INIT_HOLD_X0 -- a solve starts its state trajectory at the
+measured state x_0 instead of V's states (the reference's first-call V is zeros, ModelControl.cpp:29-50).
+Each KKT solver with the option equals the oracle with the same option (1e-9 where the iteration counts agree),
+and reaches the KKT point of the default initialisation to the stop-test accuracy (1e-7), with fewer iterations
+at the tail of the cfg#2 distribution."""
+import numpy as np
+import pytest
+
+from conftest import WEIGHTS_CFG
+
+pytestmark = pytest.mark.gpu
+
+
+def compare(g, o, tight=1e-9):
+    assert (g["status"] == 0).all() and (o["status"] == 0).all()
+    same = g["iters"] == o["iters"]
+    assert same.mean() >= 0.9
+    rel = np.abs(g["V"] - o["V"]).max(axis=1) / np.abs(o["V"]).max()
+    assert rel[same].max() < tight and rel.max() < 1e-6
+
+
+@pytest.mark.parametrize("kkt", ["condensed", "group", "lane"])
+@pytest.mark.parametrize("bounds", ["none", "u", "x"])
+def test_init_hold_matches_oracle(kkt, bounds, model_json, mmpc_mod, oracle):
+    if kkt == "condensed" and bounds == "x":
+        pytest.skip("state bounds need a Riccati solver")
+    ks = {"condensed": mmpc_mod.KKT_CONDENSED, "group": mmpc_mod.KKT_RICCATI_GROUP, "lane": mmpc_mod.KKT_RICCATI}[kkt]
+    N, h, B = 30, 0.002, 256
+    s = mmpc_mod.Solver(model_json(N=N), kkt_solver=ks, init_states=mmpc_mod.INIT_HOLD_X0, max_iter=100)
+    kw, okw = {}, {}
+    if bounds == "u":
+        kw = dict(u_lb=np.array([-3.0, -3.0]), u_ub=np.array([3.0, 3.0]))
+        okw = dict(kw)
+    elif bounds == "x":
+        xl, xu = np.array([-np.inf, -np.inf, -1.5, -1.5]), np.array([np.inf, np.inf, 1.5, 1.5])
+        s.set_state_bounds(xl, xu)
+        okw = dict(x_lb=xl, x_ub=xu)
+    x0, up, tr = oracle.synth(20250213, 0, B, N, h)
+    w = np.array(WEIGHTS_CFG)
+    g = s.solve_batch_host(x0, up, tr, w, **kw)
+    o = oracle.solve_batch(N, h, x0, up, tr, w, init_states=1, max_iter=100, **okw)
+    compare(g, o)
+    ref = oracle.solve_batch(N, h, x0, up, tr, w, max_iter=100, **okw)  # the default initialisation
+    assert np.abs(g["V"] - ref["V"]).max() / np.abs(ref["V"]).max() < 1e-7
+
+
+def test_init_hold_cuts_the_tail(model_json, mmpc_mod, oracle):
+    N, h, B = 30, 0.002, 4096
+    x0, up, tr = oracle.synth(20250213, 0, B, N, h)
+    w = np.array(WEIGHTS_CFG)
+    a = mmpc_mod.Solver(model_json(N=N)).solve_batch_host(x0, up, tr, w)
+    b = mmpc_mod.Solver(model_json(N=N, name="hold"), init_states=mmpc_mod.INIT_HOLD_X0).solve_batch_host(x0, up, tr, w)
+    assert (a["status"] == 0).all() and (b["status"] == 0).all()
+    assert b["iters"].max() < a["iters"].max() and b["iters"].mean() < a["iters"].mean()
+    assert np.abs(a["V"] - b["V"]).max() / np.abs(a["V"]).max() < 1e-7
