@@ -192,6 +192,14 @@ int mmpc_nlp_eval_batch(mmpc_handle* h, int64_t B, const double* V, const double
                         const double* traj, const double* weights, int64_t weights_stride,
                         double* J, double* defect_inf, void* stream);
 
+/* nlp_grad_f / nlp_jac_g of the reference's generated NLP (ModelGenerator.cpp:238; CasADi generate_dependencies)
+ * at V: J [B], dJ/dV [B][NV] (V layout) and the nonzero Jacobian blocks of the defects g_k = F(x_k,u_k) - x_{k+1},
+ * [dg_k/dx_k | dg_k/du_k] = [I + h df/dx | h df/du] as [B][N][nx][nx+nu] row-major (dg_k/dx_{k+1} = -I).
+ * DEVICE pointers; any output may be NULL. */
+int mmpc_nlp_derivs_batch(mmpc_handle* h, int64_t B, const double* V, const double* u_prev,
+                          const double* traj, const double* weights, int64_t weights_stride,
+                          double* J, double* grad, double* jac_blocks, void* stream);
+
 /* Synthetic instances: cfg#2 recipe for the 2-link arm, cfg#3 recipe for the exo;
  * counter-based splitmix64(seed, first_index + b), so shards generate identical instances
  * whatever the GPU count.  DEVICE pointers. */

@@ -297,6 +297,88 @@ __global__ __launch_bounds__(256) void nlp_eval_kernel(int64_t B, int N, double 
     if (ginf) ginf[b] = gm;
 }
 
+// nlp_grad_f / nlp_jac_g of the generated NLP (ModelGenerator.cpp:238, CasADi generate_dependencies): per
+// instance J, dJ/dV [NV] (V layout) and the nonzero blocks of dg/dV, [dg_k/dx_k | dg_k/du_k] = [I + h f_x | h f_u]
+// (row-major nx x (nx+nu) per stage; dg_k/dx_{k+1} = -I).  Linear mode: F_lin with A*, B* at (x_0, u_prev).
+template <class Model>
+__global__ __launch_bounds__(256) void nlp_derivs_kernel(int64_t B, int N, double h, int is_linear,
+                                                         const double* __restrict__ V, const double* __restrict__ u_prev,
+                                                         const double* __restrict__ traj,
+                                                         const double* __restrict__ weights, int64_t w_stride,
+                                                         double* J, double* grad, double* jac_blocks) {
+    constexpr int NX = Model::NX, NU = Model::NU, ND = NX + NU;
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int NV = NX * (N + 1) + NU * N;
+    const double* v = V + b * NV;
+    const double* w = weights + b * w_stride;
+    const double* up = u_prev + b * NU;
+    const double* tr = traj + b * (int64_t)N * NX;
+    double* gr = grad ? grad + b * NV : nullptr;
+    double lin[NX * NX + NX * NU + NX];
+    if (is_linear) {
+        double xd[NX], fx[NX * NX], fu[NX * NU];
+        model_eval_jac<Model>(v, up, xd, fx, fu);
+        for (int i = 0; i < NX * NX; ++i) lin[i] = fx[i];
+        for (int i = 0; i < NX * NU; ++i) lin[NX * NX + i] = fu[i];
+        for (int i = 0; i < NX; ++i) lin[NX * NX + NX * NU + i] = xd[i];
+    }
+    double Jv = 0.0;
+    if (gr)
+        for (int r = 0; r < NX; ++r) gr[N * ND + r] = 0.0;  // x_N does not enter J
+    for (int k = 0; k < N; ++k) {
+        const double* xk = v + k * ND;
+        const double* uk = xk + NX;
+        double xd[NX], fx[NX * NX], fu[NX * NU];
+        if (!is_linear) {
+            model_eval_jac<Model>(xk, uk, xd, fx, fu);
+        } else {
+            for (int r = 0; r < NX; ++r) {
+                double s = lin[NX * NX + NX * NU + r];
+                for (int c = 0; c < NX; ++c) s += lin[r * NX + c] * (xk[c] - v[c]);
+                for (int c = 0; c < NU; ++c) s += lin[NX * NX + r * NU + c] * (uk[c] - up[c]);
+                xd[r] = s;
+            }
+            for (int i = 0; i < NX * NX; ++i) fx[i] = lin[i];
+            for (int i = 0; i < NX * NU; ++i) fu[i] = lin[NX * NX + i];
+        }
+        double qe[NX];
+        for (int r = 0; r < NX; ++r) {
+            const double e = xk[r] + h * xd[r] - tr[k * NX + r];
+            Jv += e * w[r] * e;
+            qe[r] = 2.0 * w[r] * e;
+        }
+        if (jac_blocks) {
+            double* jb = jac_blocks + (b * N + k) * (int64_t)(NX * ND);
+            for (int r = 0; r < NX; ++r) {
+                for (int c = 0; c < NX; ++c) jb[r * ND + c] = (r == c ? 1.0 : 0.0) + h * fx[r * NX + c];
+                for (int c = 0; c < NU; ++c) jb[r * ND + NX + c] = h * fu[r * NU + c];
+            }
+        }
+        for (int c = 0; c < NU; ++c) {
+            const double um = (k == 0) ? up[c] : v[(k - 1) * ND + NX + c];
+            const double du = uk[c] - um;
+            Jv += du * w[NX + c] * du + uk[c] * w[NX + NU + c] * uk[c];
+        }
+        if (gr) {
+            for (int c = 0; c < NX; ++c) {  // dJ/dx_k = 2 (I + h f_x)^T Q e_k
+                double t = qe[c];
+                for (int r = 0; r < NX; ++r) t += h * fx[r * NX + c] * qe[r];
+                gr[k * ND + c] = t;
+            }
+            for (int c = 0; c < NU; ++c) {  // dJ/du_k = 2 h f_u^T Q e_k + Delta-u and Rm terms
+                double t = 0.0;
+                for (int r = 0; r < NX; ++r) t += h * fu[r * NU + c] * qe[r];
+                const double um = (k == 0) ? up[c] : v[(k - 1) * ND + NX + c];
+                t += 2.0 * w[NX + c] * (uk[c] - um) + 2.0 * w[NX + NU + c] * uk[c];
+                if (k + 1 < N) t -= 2.0 * w[NX + c] * (v[(k + 1) * ND + NX + c] - uk[c]);
+                gr[k * ND + NX + c] = t;
+            }
+        }
+    }
+    if (J) J[b] = Jv;
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -912,6 +994,32 @@ int mmpc_nlp_eval_batch(mmpc_handle* h, int64_t B, const double* V, const double
         nlp_eval_kernel<M><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
             B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
             weights_stride, J, defect_inf);
+        return MMPC_OK;
+    });
+    if (rc) return rc;
+    MMPC_HIP(hipGetLastError());
+    return MMPC_OK;
+}
+
+int mmpc_nlp_derivs_batch(mmpc_handle* h, int64_t B, const double* V, const double* u_prev, const double* traj,
+                          const double* weights, int64_t weights_stride, double* J, double* grad, double* jac_blocks,
+                          void* stream) {
+    if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!V || !u_prev || !traj || !weights) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    const int nw = h->info.num_x + 2 * h->info.num_u;
+    if (weights_stride != 0 && weights_stride < nw) return fail(MMPC_ERR_INVALID_ARG, "weights_stride must be 0 or >= nx+2nu");
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    rc = with_model(h->info.model_id, [&](auto* m) {
+        using M = std::remove_pointer_t<decltype(m)>;
+        nlp_derivs_kernel<M><<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
+            weights_stride, J, grad, jac_blocks);
         return MMPC_OK;
     });
     if (rc) return rc;

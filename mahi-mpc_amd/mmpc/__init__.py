@@ -107,6 +107,7 @@ def lib(path: str | None = None):
         L.mmpc_linearize_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 5
         L.mmpc_nlp_eval_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 3
         L.mmpc_synth_batch.argtypes = [_vp, C.c_uint64, C.c_int64, C.c_int64] + [_vp] * 4
+        L.mmpc_nlp_derivs_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 4
         L.mmpc_resolve_kkt_solver.argtypes = [_vp, C.c_int64, C.POINTER(C.c_int32)]
         L.mmpc_set_state_bounds.argtypes = [_vp, _vp, _vp]
         L.mmpc_get_state_bounds.argtypes = [_vp, _vp, _vp]
@@ -258,6 +259,12 @@ class Solver:
     def nlp_eval(self, B, V, u_prev, traj, weights, J, defect_inf, weights_stride=0, stream=None):
         self._check(self._L.mmpc_nlp_eval_batch(self._h, B, _ptr(V), _ptr(u_prev), _ptr(traj), _ptr(weights),
                                          weights_stride, _ptr(J), _ptr(defect_inf), stream))
+
+    def nlp_derivs(self, B, V, u_prev, traj, weights, J=None, grad=None, jac_blocks=None, weights_stride=0,
+                   stream=None):
+        """J, dJ/dV and the defect-Jacobian stage blocks at V (device pointers; nlp_grad_f / nlp_jac_g)."""
+        self._check(self._L.mmpc_nlp_derivs_batch(self._h, B, _ptr(V), _ptr(u_prev), _ptr(traj), _ptr(weights),
+                                                  weights_stride, _ptr(J), _ptr(grad), _ptr(jac_blocks), stream))
 
     def linearize(self, B, x, u, A, Bm, xdot, stream=None):
         self._check(self._L.mmpc_linearize_batch(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xdot), stream))
