@@ -1,25 +1,35 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X batched NMPC solve path (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 4096] [--horizon 30]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2|cfg3|cfg5] [--batch B] [--horizon N]
 
-One "step" = one cold-started batched SQP solve of B independent cfg#2 instances (2-link arm,
-nx=4, nu=2, N=30, h=2 ms, fp64), i.e. what the reference does per control tick in
-ModelControl::calc_u (src/Mahi/Mpc/ModelControl.cpp:116-172) -- from V = 0 with x_0 pinned, the
-reference's first-call state -- for B instances at once.  Inputs are generated on the device from
-(seed, global instance index) before the timed region (weak scaling: every rank solves its own
-B instances; results are independent of the GPU count).
+One "step" = one cold-started batched SQP solve of B independent instances per GPU (cfg#2: 2-link arm, nx=4,
+nu=2, N=30, h=2 ms, fp64), i.e. what the reference does per control tick in ModelControl::calc_u
+(src/Mahi/Mpc/ModelControl.cpp:116-172) -- from V = 0 with x_0 pinned, the reference's first-call state -- for
+B instances at once, THROUGH RESULTS ON HOST: every step ends with the per-instance results the
+reference consumes (u_0*, status, iterations; ModelControl.cpp:160-190) copied into pinned host memory (N > 1:
+gathered to rank 0 over RCCL first, then copied to rank 0's host).  Inputs are generated on the device from
+(seed, global instance index) before the timed region (weak scaling: rank r solves global instances
+[r B, (r+1) B); results do not depend on the GPU count).
+
+Multi-GPU: ``--gpus N`` with N > 1 and no WORLD_SIZE in the environment makes this process a launcher that
+starts N rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each) before anything touches
+the GPU, forwards rank 0's JSON line and exits with the worst rank exit code.  Under torchrun (WORLD_SIZE set)
+the process is a rank itself.
 
 Prints ONE JSON line on rank 0 (driver contract) with two extra objects:
-  roofline      achieved algorithmic FP64 rate of the fused SQP kernel vs the MI355X FP64 peak,
-                kernel time from HIP events on the launch stream;
-  cpu_baseline  the oracle/ CPU restatement (same GN-SQP, fp64) on a bounded sample, rank 0 only.
+  roofline      the dominant kernel's achieved FP64 rate (its own algorithmic flop count) vs the MI355X FP64
+                vector peak; kernel time from HIP events on the launch stream;
+  cpu_baseline  the oracle/ CPU restatement (same GN-SQP NLP, fp64) on a bounded sample, rank 0 at N = 1 only,
+                with its agreement with the GPU solutions and both iteration histograms.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -34,91 +44,185 @@ SEED = 20250213
 WEIGHTS = [10.0, 1.0, 5.0, 5.0, 5.0, 5.0, 0.01, 0.01]
 # SURVEY.md 8d cfg#3 (exo): Q = [10 x4, 1 x4], R = 1 x4, Rm = 0.01 x4
 WEIGHTS_EXO = [10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4
+_EXO_METRIC = "MPC solves/sec (whole node), exo nx=8 N=50 batch (SURVEY.md 8d cfg#3/#4)"
 CONFIGS = {
-    "cfg2": dict(model="two_link_arm", nx=4, nu=2, N=30, B=4096, weights=WEIGHTS, metric=METRIC,
+    "cfg2": dict(model="two_link_arm", nx=4, nu=2, N=30, B=4096, weights=WEIGHTS, metric=METRIC, fp32=False,
                  workload="cfg#2: 2-link arm nx=4 nu=2, N=30, h=2 ms, cold-start GN-SQP to ||grad||<=1e-8, ||g||<=1e-10"),
-    "cfg3": dict(model="exo_arm", nx=8, nu=4, N=50, B=65536, weights=WEIGHTS_EXO,
-                 metric="MPC solves/sec (whole node), exo nx=8 N=50 batch (SURVEY.md 8d cfg#3/#4)",
+    "cfg3": dict(model="exo_arm", nx=8, nu=4, N=50, B=65536, weights=WEIGHTS_EXO, metric=_EXO_METRIC, fp32=False,
                  workload="cfg#3: 4-DoF exo nx=8 nu=4 (build-defined parameters), N=50, h=2 ms, cold-start GN-SQP "
                           "(Riccati KKT) to ||grad||<=1e-8, ||g||<=1e-10"),
+    "cfg5": dict(model="exo_arm", nx=8, nu=4, N=50, B=65536, weights=WEIGHTS_EXO, fp32=True,
+                 metric="MPC solves/sec (whole node), exo nx=8 N=50 batch, fp32 KKT factor + fp64 residuals "
+                        "(SURVEY.md 8d cfg#5)",
+                 workload="cfg#5: cfg#3 with the Riccati matrix recursion in fp32 and every right-hand side, "
+                          "residual, model evaluation and merit in fp64 (each SQP iteration = one refinement "
+                          "step), to ||grad||<=1e-8, ||g||<=1e-10"),
 }
-FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector = FP64 matrix peak (AMD spec)
-HBM_PEAK_GBS = 8000.0
+FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (AMD spec); FP64 matrix peak is the same
+FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md chip table)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="cfg2",
-                    help="cfg2 = headline (BASELINE.json); cfg3 = exo workload of SURVEY.md 8d")
-    ap.add_argument("--batch", type=int, default=None, help="instances per GPU (cfg#2: 4096, cfg#3: 65536)")
+                    help="cfg2 = headline (BASELINE.json); cfg3 / cfg5 = exo workloads of SURVEY.md 8d")
+    ap.add_argument("--batch", type=int, default=None, help="instances per GPU (cfg#2: 4096, cfg#3/#5: 65536)")
     ap.add_argument("--kkt", choices=["auto", "condensed", "riccati", "group"], default="auto",
                     help="KKT solver (mmpc_opts.kkt_solver); auto = the library's choice")
     ap.add_argument("--horizon", type=int, default=None)
-    ap.add_argument("--no-gather", action="store_true", help="N > 1: skip gathering the results to rank 0")
+    ap.add_argument("--tol", type=float, default=None,
+                    help="outer tolerance: tol_grad = tol, tol_defect = tol/100 (default: 1e-8 / 1e-10)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--init", choices=["as_given", "hold_x0"], default="as_given",
                     help="mmpc_opts.init_states: the reference's cold start (V = 0) or x_1..x_N = x_0 (DESIGN 3d)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch per config (tools/pmc.sh + tools/pmc_summary.py)")
-    return ap.parse_args()
+    ap.add_argument("--standin", action="store_true",
+                    help="TEST ONLY: CPU tensors, gloo and a trivial stand-in solver, to exercise the launcher / "
+                         "rank / gather plumbing without a GPU (tests/test_bench_launch.py); never a measurement")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(cfg, N, h, target_s):
-    """Oracle (oracle/liboracle.so, the same GN-SQP in plain C + OpenMP) on a bounded sample."""
+# ------------------------------------------------------------------ launcher (N > 1, no torchrun)
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args, argv) -> int:
+    """Start one rank process per GPU and wait for all of them.  Nothing here initialises the GPU (no torch,
+    no mmpc import): each child is a fresh interpreter that sees every device and picks LOCAL_RANK."""
+    n = args.gpus
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, p in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):   # one rank failed: the others would hang in a collective
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    p.kill()
+                    rcs[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [rc for rc in rcs if rc]
+    return (bad[0] if bad[0] > 0 else 1) if bad else 0
+
+
+# ------------------------------------------------------------------ CPU baseline (rank 0, N = 1 only)
+def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect):
+    """Oracle (oracle/liboracle.so: the same NLP and GN-SQP in plain C + OpenMP, dense condensed KKT) on a
+    bounded sample of the same seeded workload, plus its agreement with the GPU on the shared instances."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as o
     model = o.EXO if cfg["model"] == "exo_arm" else o.TWO_LINK
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     w = np.array(cfg["weights"])
+    kw = dict(nthreads=threads, model=model, tol_grad=tol_grad, tol_defect=tol_defect)
     n0 = 2 * threads
     x0, up, tr = o.synth(SEED, 0, n0, N, h, model=model)
     t = time.perf_counter()
-    o.solve_batch(N, h, x0, up, tr, w, nthreads=threads, model=model)
+    o.solve_batch(N, h, x0, up, tr, w, **kw)
     dt = time.perf_counter() - t
     n = int(max(n0, min(200000, n0 * target_s / max(dt, 1e-6))))
     x0, up, tr = o.synth(SEED, 0, n, N, h, model=model)
     t = time.perf_counter()
-    r = o.solve_batch(N, h, x0, up, tr, w, nthreads=threads, model=model)
+    r = o.solve_batch(N, h, x0, up, tr, w, **kw)
     dt = time.perf_counter() - t
+    m = min(n, gpu_V.shape[0])
+    ref = r["V"][:m]
+    scale = np.maximum(np.abs(ref).max(axis=1), 1e-300)
+    rel = np.abs(gpu_V[:m] - ref).max(axis=1) / scale
+    same_it = r["iters"][:m] == gpu_iters[:m]
+    hist = lambda a: {int(k): int(v) for k, v in zip(*np.unique(a, return_counts=True))}  # noqa: E731
     return dict(value=n / dt, unit="solves/s", cores=threads, kind="port",
                 sample=f"first {n} {cfg['workload'].split(':')[0]} instances (seed {SEED}), cold start, {dt:.1f} s "
-                       f"wall, {int((r['status'] == 0).sum())}/{n} converged, oracle dense condensed GN-SQP, "
-                       f"{threads} OpenMP threads")
+                       f"wall, {int((r['status'] == 0).sum())}/{n} converged; oracle GN-SQP with a DENSE condensed "
+                       f"KKT (Cholesky of the N*nu Hessian, not the Riccati recursion the GPU runs), "
+                       f"{threads} OpenMP threads",
+                vs_gpu=dict(instances=int(m), max_rel_diff_V=float(rel.max()),
+                            max_rel_diff_V_same_iters=float(rel[same_it].max()) if same_it.any() else None,
+                            same_iteration_count=int(same_it.sum())),
+                iters_hist_cpu=hist(r["iters"]), iters_hist_gpu=hist(gpu_iters))
 
 
-def main():
-    args = parse()
+# ------------------------------------------------------------------ test stand-in (no GPU)
+class _StandInSolver:
+    """--standin only: a CPU 'solver' with the mmpc.Solver call shape whose outputs are a fixed function of the
+    synthetic inputs (u_0* := x0[:, :nu], status 0, iters 1), so the launcher / rank / gather plumbing can be
+    tested on gloo.  It is not the solve path and never produces a reported number."""
+
+    def __init__(self, nx, nu, N):
+        self.nx, self.nu, self.N, self.NV = nx, nu, N, nx * (N + 1) + nu * N
+
+    def synth(self, seed, first, B, x0, up, tr, stream=None):
+        import torch
+        idx = torch.arange(first, first + B, dtype=torch.float64)[:, None]
+        x0.copy_(idx + torch.arange(self.nx, dtype=torch.float64) / 10)
+        up.zero_()
+        tr.zero_()
+
+    def solve_batch(self, B, x0, up, tr, w, V, st, it, kkt, stream=None):
+        V.zero_()
+        V[:, self.nx:self.nx + self.nu] = x0[:, :self.nu]
+        st.zero_()
+        it.fill_(1)
+        kkt.zero_()
+
+
+# ------------------------------------------------------------------ one rank
+def run_rank(args):
     import torch
     import torch.distributed as dist
-    import mmpc
     import mmpc.dist as mdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    standin = args.standin
     if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        dist.init_process_group("gloo" if standin else "nccl")
     cfg = CONFIGS[args.config]
     B = args.batch or cfg["B"]
     N = args.horizon or cfg["N"]
     nx, nu, h_us = cfg["nx"], cfg["nu"], 2000
     h = h_us * 1e-6
+    tol_grad = 1e-8 if args.tol is None else args.tol
+    tol_defect = 1e-10 if args.tol is None else args.tol / 100
 
-    tmpdir = tempfile.mkdtemp(prefix="mmpc_bench_")
-    path = mmpc.write_model_json(os.path.join(tmpdir, f"{cfg['model']}.json"), cfg["model"], nx, nu, h_us, N,
-                                 model=cfg["model"])
-    ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt]
-    solver = mmpc.Solver(path, device=local, kkt_solver=ksolver,
-                         init_states=mmpc.INIT_HOLD_X0 if args.init == "hold_x0" else mmpc.INIT_AS_GIVEN)
-    solver.reserve_workspace(B)
-    ksolver = solver.kkt_solver_for(B)   # the AUTO choice, resolved by the library
-    riccati = ksolver in (2, 3)
+    if standin:
+        dev = torch.device("cpu")
+        solver = _StandInSolver(nx, nu, N)
+        ksolver = 0
+        stream = None
+    else:
+        import mmpc
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        tmpdir = tempfile.mkdtemp(prefix="mmpc_bench_")
+        path = mmpc.write_model_json(os.path.join(tmpdir, f"{cfg['model']}.json"), cfg["model"], nx, nu, h_us, N,
+                                     model=cfg["model"])
+        ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt]
+        solver = mmpc.Solver(path, device=local, kkt_solver=ksolver, factor_fp32=cfg["fp32"],
+                             tol_grad=tol_grad, tol_defect=tol_defect,
+                             init_states=mmpc.INIT_HOLD_X0 if args.init == "hold_x0" else mmpc.INIT_AS_GIVEN)
+        solver.reserve_workspace(B)
+        ksolver = solver.kkt_solver_for(B)   # the AUTO choice, resolved by the library
+        stream = torch.cuda.current_stream(dev)
     NV = solver.NV
     f64 = dict(dtype=torch.float64, device=dev)
     x0 = torch.empty((B, nx), **f64)
@@ -129,79 +233,76 @@ def main():
     st = torch.empty(B, dtype=torch.int32, device=dev)
     it = torch.empty(B, dtype=torch.int32, device=dev)
     kkt = torch.empty(B, **f64)
-    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream if stream is not None else None
     first, _ = mdist.shard(B, rank)
-    solver.synth(SEED, first, B, x0, up, tr, stream=stream.cuda_stream)
+    solver.synth(SEED, first, B, x0, up, tr, stream=sh)
     mdist.broadcast_shared(w)   # shared weights from rank 0 (identical here by construction)
-    # N > 1: every step's per-instance results (u_0*, status, iterations) go to rank 0 -- one RCCL
-    # all_gather_into_tensor over xGMI per step, issued async so it overlaps the next step's solve
-    gather = mdist.ResultGather(B, nx, nu) if (world > 1 and not args.no_gather) else None
 
-    def step():
+    # results the reference consumes per tick: u_0* (ModelControl.cpp:174-190), status, iterations
+    ncol = nu + 2
+    pack = torch.empty((B, ncol), **f64)
+    table = torch.empty((world * B, ncol), **f64) if world > 1 else pack
+    pin = dict(pin_memory=True) if not standin else {}
+    host = [torch.empty((world * B, ncol), dtype=torch.float64, **pin) for _ in range(2)]
+
+    def results_to_host(k):
+        pack[:, :nu] = V[:, nx:nx + nu]
+        pack[:, nu] = st
+        pack[:, nu + 1] = it
+        if world > 1:   # N > 1: one all_gather_into_tensor (RCCL over xGMI) to rank 0's device, then D2H there
+            dist.all_gather_into_tensor(table, pack, async_op=True).wait()   # stream-ordered on GPUs
+        if rank == 0:
+            host[k % 2].copy_(table, non_blocking=not standin)
+
+    def solve():
         V.zero_()   # cold start (reference first call: v_init = 0, ModelControl.cpp:29-50)
-        solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=stream.cuda_stream)
+        solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=sh)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for k in range(args.warmup):
+        solve()
+        results_to_host(k)
+    sync = (lambda: torch.cuda.synchronize(dev)) if not standin else (lambda: None)
+    sync()
+    ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+          if not standin else None)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        V.zero_()
-        ev[k][0].record(stream)
-        solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=stream.cuda_stream)
-        ev[k][1].record(stream)
-        if gather:
-            gather.post(V, st, it)
-    if gather:
-        gather.wait()
-    torch.cuda.synchronize(dev)
+        if ev:
+            V.zero_()
+            ev[k][0].record(stream)
+            solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=sh)
+            ev[k][1].record(stream)
+        else:
+            solve()
+        results_to_host(k)
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else 0.0
     elapsed = mdist.max_over_ranks(elapsed, device=dev)
 
     iters = it.cpu().numpy()
     status = st.cpu().numpy()
-    if gather:   # rank 0 holds every instance's result of the last step
-        last = gather.last()
-        gathered_ok = bool(torch.equal(last[rank * B:(rank + 1) * B, :nu], V[:, nx:nx + nu]))
+    # rank 0's host table of the last step against every rank's own results
+    mine = pack.cpu()
+    ok = True
+    if rank == 0:
+        last = host[(args.steps - 1) % 2]
+        ok = bool(torch.equal(last[:B], mine))
         conv = int((last[:, nu] == 0).sum().item())
-        gathered_ok = bool(mdist.sum_over_ranks(int(not gathered_ok), device=dev) == 0)
+        tail = last
     else:
-        conv = int(mdist.sum_over_ranks(int((status == 0).sum()), device=dev))
+        conv = 0
+        tail = None
+    if world > 1:
+        ok = bool(torch.equal(table[rank * B:(rank + 1) * B].cpu(), mine)) and ok
+        ok = mdist.sum_over_ranks(int(not ok), device=dev if not standin else None) == 0
     total = B * world * args.steps
     value = total / elapsed
-    # algorithmic flops of one launch = per-iteration figure x the SQP iterations the launch's instances
-    # actually took (unit of work = 1 solve = sum over its iterations), SURVEY.md 8(d)'s figure whichever KKT
-    # solver ran -- except where that figure (which prices the condensed algorithm: 9.3 MFLOP/iter at cfg#3)
-    # would put a Riccati kernel above the FP64 peak; there the kernel's own algorithmic count is used
-    # (both are reported).
-    survey_fl = float(iters.sum()) * mmpc.survey_flops_per_iteration(N, nx, nu)
-    survey_tf = survey_fl / (kern_ms * 1e-3) / 1e12
-    if riccati:
-        fl = mmpc.riccati_flops_per_iteration(N, nx, nu)
-        own_fl = float(iters.sum()) * fl["total"]
-        achieved = survey_tf if survey_tf <= FP64_PEAK_TFLOPS else own_fl / (kern_ms * 1e-3) / 1e12
-        kname = (f"sqp_{'group' if ksolver == 3 else 'lane'}_kernel<"
-                 f"{'ExoArm' if cfg['model'] == 'exo_arm' else 'TwoLinkArm'}>")
-    else:
-        fl = mmpc.flops_per_iteration(N)
-        own_fl = float(iters.sum()) * fl["total"]
-        achieved = survey_fl / (kern_ms * 1e-3) / 1e12
-        kname = f"sqp_wave_kernel<TwoLinkArm,{30 if 16 < N <= 30 else (16 if N <= 16 else 32)}>"
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json)).get(f"{args.config}:{kname}", {})
-            if tj.get("batch") == B and tj.get("horizon") == N:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
     out = {
         "metric": cfg["metric"],
         "value": value,
@@ -213,35 +314,95 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
-        "data": f"synthetic: counter-based splitmix64 {args.config} instances (SURVEY.md 8d), generated on device",
+        "dtype": "f64" if not cfg["fp32"] else "f64 (fp32 Riccati factor)",
+        "data": f"synthetic: counter-based splitmix64 {args.config} instances (SURVEY.md 8d), generated on device "
+                f"from (seed, global instance index), so N = 1 and N > 1 solve identical instances",
         "config": {"workload": cfg["workload"], "batch_per_gpu": B, "global_batch": B * world,
-                   "horizon": N, "kkt_solver": {1: "condensed (wave per instance)", 2: "riccati (lane per instance)",
-                                                3: "riccati (16 lanes per instance)"}[ksolver],
+                   "horizon": N, "tol_grad": tol_grad, "tol_defect": tol_defect,
+                   "kkt_solver": {0: "stand-in (test)", 1: "condensed (wave per instance)",
+                                  2: "riccati (lane per instance)", 3: "riccati (16 lanes per instance)"}[ksolver],
                    "init_states": "V as given (reference cold start V = 0)" if args.init == "as_given"
                    else "x_1..x_N = x_0 (MMPC_INIT_HOLD_X0)",
-                   "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) to rank 0 by "
-                                   "RCCL all_gather_into_tensor, overlapped with the next solve"
-                                   if gather else f"batch-shard x{world} (no collective on the solve path)")},
+                   "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) gathered to "
+                                   "rank 0 by RCCL all_gather_into_tensor, then D2H into pinned memory"
+                                   if world > 1 else "batch-shard x1; per-step results D2H into pinned memory"),
+                   "timed_region": "cold-start solve + results (u_0*, status, iters) on rank 0's host"},
         "converged": conv,
-        **({"gathered_results_match": gathered_ok} if gather else {}),
+        "gathered_results_match": ok,
         "mean_sqp_iters": float(iters.mean()),
-        "kernel_ms": kern_ms,
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                     "kernel": kname,
-                     "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N, nx, nu),
-                     "flops_per_iter_kernel_own_count": fl["total"],
-                     "kernel_own_count_tflops": own_fl / (kern_ms * 1e-3) / 1e12,
-                     "survey_8d_equivalent_tflops": survey_fl / (kern_ms * 1e-3) / 1e12},
+        "max_sqp_iters": int(iters.max()),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds)
+    if standin:
+        out["standin"] = True
+        if tail is not None:
+            out["standin_u0_first_col"] = tail[:, 0].tolist()
+    else:
+        import mmpc
+        out["kernel_ms"] = kern_ms
+        out["roofline"] = roofline(args, cfg, mmpc, ksolver, N, nx, nu, B, iters, kern_ms)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin:
+        out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
+                                           tol_defect)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    solver.close()
+    if not standin:
+        solver.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def roofline(args, cfg, mmpc, ksolver, N, nx, nu, B, iters, kern_ms):
+    """FP64-VALU roofline of the solve kernel (the only kernel of a step besides a memset and the result pack).
+
+    achieved = the kernel's OWN algorithmic flop count (mmpc.*_flops_per_iteration: structure-exploiting, no
+    flop on structural zeros, model evaluations excluded) x the SQP iterations its instances took / the mean
+    kernel duration (HIP events on the launch stream).  peak = FP64 vector peak (no kernel issues MFMA: DESIGN.md
+    "Why no MFMA"; cfg#5 prices its fp32 share at the fp64 peak, i.e. conservatively high).  The SURVEY.md 8(d)
+    count (explicit condensing + dense Cholesky, 288 kflop/iter at cfg#2) is reported beside it as the
+    algorithm-equivalent rate: it is NOT the work the kernel does."""
+    riccati = ksolver in (2, 3)
+    if riccati:
+        fl = mmpc.riccati_flops_per_iteration(N, nx, nu)
+        model = "ExoArm" if cfg["model"] == "exo_arm" else "TwoLinkArm"
+        if ksolver == 3:
+            kname = f"sqp_group_kernel<{model}"
+        else:
+            kname = f"sqp_lane_kernel<{model}"
+    else:
+        fl = mmpc.flops_per_iteration(N)
+        kname = f"sqp_wave_kernel<TwoLinkArm,{30 if 16 < N <= 30 else (16 if N <= 16 else 32)}>"
+    sec = kern_ms * 1e-3
+    own = float(iters.sum()) * fl["total"] / sec / 1e12
+    survey = float(iters.sum()) * mmpc.survey_flops_per_iteration(N, nx, nu) / sec / 1e12
+    traffic = None
+    key = f"{args.config}:{kname}"
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json)).get(key, {})
+            if tj.get("batch") == B and tj.get("horizon") == N:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    alg_bytes = B * (8 * (nx + nu + N * nx + 2 * (nx * (N + 1) + nu * N)) + 12)   # SURVEY.md 8d, per launch
+    return {"bound": "fp64-valu", "achieved": own, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": own / FP64_PEAK_TFLOPS, "traffic": traffic,
+            "kernel": kname,
+            "flops_per_iter_kernel_own_count": fl["total"],
+            "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N, nx, nu),
+            "survey_8d_equivalent_tflops": survey,
+            "survey_8d_equivalent_frac": survey / FP64_PEAK_TFLOPS,
+            "algorithmic_hbm_bytes_per_launch": alg_bytes,
+            "hbm_gbs_algorithmic": alg_bytes / sec / 1e9,
+            "mfma_instructions": 0,
+            "note": "frac = kernel's own flops / FP64 vector peak; MFMA/FP64-VALU counters: profiles/r02/"}
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args, argv))
+    run_rank(args)
 
 
 if __name__ == "__main__":

@@ -14,6 +14,8 @@
 // LDS per instance (fp64): x_k, u_k, F_k, c_k, hFq_k, hFqd_k, hFu_k, d_k, dx_k, du_k (cross-lane data); the
 // targets stay in HBM (read-only) and the gains K_k in a per-instance HBM workspace (serial lane only).
 #pragma once
+#include <type_traits>
+
 #include "models.h"
 #include "sqp_lane.h"
 #include "sqp_wave.h"
@@ -57,6 +59,25 @@ __device__ __forceinline__ double group_max(double v) {
 }
 __device__ __forceinline__ double group_bcast(double v, int base) { return __shfl(v, base); }
 __device__ __forceinline__ int group_bcast_i(int v, int base) { return __shfl(v, base); }
+
+// Lane L of every 16-lane row (= one instance group) to the whole row: one v_mov_b64_dpp row_newbcast:L
+// (gfx950 DPP64).  Measured on MI355X (tools/ubench/f64_latency.hip): a dependent FMA through it costs
+// 17 cycles against 11 for a plain dependent FMA and ~80 through __shfl (ds_bpermute) or an LDS round trip,
+// so the lane-distributed Riccati sweep below exchanges data with it.
+template <int L>
+__device__ __forceinline__ double row_bcast(double v) {
+    static_assert(L >= 0 && L < 16, "row lane");
+    // bound_ctrl with full row/bank masks: every lane is written, so the old value is dead (no copy)
+    return __builtin_amdgcn_update_dpp(v, v, 0x150 + L, 0xf, 0xf, true);
+}
+// compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1 (row_bcast needs a constant lane)
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        sfor<B + 1, E>(static_cast<F&&>(f));
+    }
+}
 
 // xd = f(x, u); with jac also the acceleration partials (unscaled).  Linear mode (ModelGenerator.cpp:47-48):
 // F_lin with the acceleration Jacobians lFq, lFqd, lFu and xdot lxd taken at (lxs, lus).
@@ -159,6 +180,32 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     }
     double lbv[NU], ubv[NU];
     load_bounds<NU, BOUNDED>(p, lbv, ubv);
+    // ---- lane-distributed Riccati (DIST): lane r of the group owns row r of the augmented value function
+    //      P~ (NS x NS) and of every per-row quantity; small per-stage quantities are computed redundantly on
+    //      all lanes; rows are exchanged with row_bcast.  Bounded / state-bounded solves keep
+    //      the one-lane sweep below. ----
+    constexpr bool DIST = (NS < G) && !BOUNDED && !XB;
+    const int r = gl;
+    const bool lx = r < NX, lu = r >= NX && r < NS, la = r >= NQ && r < NX;
+    const int rx = lx ? r : 0;                        // x row of this lane (clamped for address arithmetic)
+    const int ru = lu ? r - NX : 0;                   // u row
+    const int ta = la ? r - NQ : 0;                   // row of the a-blocks (hFq, hFqd, hFu) of an a-lane
+    const double Qr = lx ? w[rx] : 0.0;               // Q of this lane's x row
+    // lane-role masks as blend factors: the DIST loops blend loaded values with FMAs instead of selects (a select
+    // of an LDS load becomes a branch or a pointer select)
+    const double lqd = r < NQ ? 1.0 : 0.0, lad = la ? 1.0 : 0.0;
+    const int rq = r < NQ ? r : 0;                    // q column of a q-lane (clamped)
+    const double Rr = lu ? w[NX + ru] : 0.0;          // R of this lane's u row
+    double hq[NQ > 0 ? NQ : 1], hrow[NX], qoh[NX], rdg[NU];
+#pragma unroll
+    for (int z = 0; z < NQ; ++z) hq[z] = (r == NQ + z) ? h : 0.0;   // column r of A holds h in row z (kinematics)
+#pragma unroll
+    for (int j = 0; j < NX; ++j) {
+        hrow[j] = (r < NQ && j == NQ + r) ? h : 0.0;  // row r of A of a q-lane (besides the identity)
+        qoh[j] = (j == r) ? Qr : 0.0;
+    }
+#pragma unroll
+    for (int c = 0; c < NU; ++c) rdg[c] = (r == NX + c) ? R[c] : 0.0;
     // ---- load: V (reference layout) -> LDS, x_0 pinned (ModelControl.cpp:144-145) ----
     {
         const double* Vin = p.V + ii * (int64_t)NV;
@@ -222,6 +269,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     bool done = !valid;
     MMPC_PHASE(0);
     for (it = 0; !done; ++it) {
+        MMPC_PHASE(8);
         __builtin_amdgcn_wave_barrier();
         // ---- A. stage-parallel: F_k, A_k/B_k blocks, defects, merit value ----
         double J0 = 0.0, c1 = 0.0, cmax = 0.0;
@@ -664,7 +712,328 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             }
 #undef GROUP_LOAD_STEP
         };
-        if (gl == 0) {
+        // ---- DIST: the same recursions with row r of every quantity on lane r of the group ----
+        // column r of A (x-lanes): own row (identity) + h in row z for r = NQ + z + acol[t] in row NQ + t, where
+        // acol = hFq[:, r] (q-lanes) or hFqd[:, r - NQ] (a-lanes); so (A^T v)[r] = colA(v_r, vb) with vb = all v.
+        auto colA = [&](double own, const double* acol, const double* vb) {
+            double t = lx ? own : 0.0;
+#pragma unroll
+            for (int z = 0; z < NQ; ++z) t = fma(hq[z], vb[z], t);
+#pragma unroll
+            for (int s2 = 0; s2 < NA; ++s2) t = fma(acol[s2], vb[NQ + s2], t);
+            return t;
+        };
+        // row r of [A - I | B] (x-lanes) at stage k: q-lanes h e_{NQ+r}, a-lanes [hFq, hFqd | hFu] row r - NQ
+        // (loads are unconditional from clamped rows and then selected: a conditional LDS load becomes a branch)
+        // (the asm pins keep the selects on values: select(load, hrow[j]) otherwise becomes a flat load through a
+        // selected LDS-or-scratch pointer)
+        auto load_arow = [&](int k, double* arow, double* brow) {
+#pragma unroll
+            for (int s2 = 0; s2 < NQ; ++s2) arow[s2] = fma(lad, sFq[k * FQ + ta * NQ + s2], hrow[s2]);
+#pragma unroll
+            for (int s2 = 0; s2 < NA; ++s2) arow[NQ + s2] = fma(lad, sFqd[k * FD + ta * NA + s2], hrow[NQ + s2]);
+#pragma unroll
+            for (int c = 0; c < NU; ++c) brow[c] = lad * sFu[k * FU + ta * NU + c];
+        };
+        // d_{k+1} = A_k d_k + c_k (d_0 = 0): lane r holds d_k[r]
+        // The recursions below are latency-bound (a few FMAs per stage on the dependency chain): every stage's
+        // LDS operands are loaded one stage ahead and the dot products split into two partial sums.
+        auto d_recursion_dist = [&]() {
+            double dr = 0.0;
+            if (lx) sD[rx] = 0.0;
+            double na[NX], nc;
+            {
+                double nb[NU];
+                load_arow(0, na, nb);
+                nc = sC[rx];
+            }
+#pragma unroll 2
+            for (int k = 0; k < N; ++k) {
+                double db[NX], arow[NX];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) arow[j] = na[j];
+                const double cr = nc;
+                {
+                    const int kn = k + 1 < N ? k + 1 : k;
+                    double nb[NU];
+                    load_arow(kn, na, nb);
+                    nc = sC[kn * NX + rx];
+                }
+                sfor<0, NX>([&](auto I) { db[I] = row_bcast<I>(dr); });
+                double t0 = dr + cr, t1 = 0.0;
+#pragma unroll
+                for (int j = 0; j < NX; ++j) {
+                    if (j & 1) t1 = fma(arow[j], db[j], t1);
+                    else t0 = fma(arow[j], db[j], t0);
+                }
+                dr = lx ? t0 + t1 : 0.0;
+                if (lx) sD[(k + 1) * NX + rx] = dr;
+            }
+        };
+        // adjoint + reduced gradient + Riccati backward sweep; lane r: row r of P~ (Prow) and p~ (pvr), lam[r]
+        // column r of the a-rows of A at stage k: hFq[:, r] (q-lanes), hFqd[:, r - NQ] (a-lanes), 0 otherwise
+        auto load_acol = [&](int k, double* acol) {
+#pragma unroll
+            for (int t2 = 0; t2 < NA; ++t2) {
+                double v = lad * sFqd[k * FD + t2 * NA + ta];
+                if constexpr (NQ > 0) v = fma(lqd, sFq[k * FQ + t2 * NQ + rq], v);
+                acol[t2] = v;
+            }
+        };
+        // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1} (lam_N = Q e_{N-1}, e_{k-1} = d_k + x_k - r_{k-1}) and the
+        // reduced gradient g_k = B_k^T lam_{k+1} + R (u_k - u_{k-1}) + Rm u_k - R (u_{k+1} - u_k): lane r holds
+        // lam[r] (x-lanes) and g_k[r - NX] (u-lanes); gmax, lmax are per-lane maxima (reduced by the caller).
+        // Runs before the stop test, so a converged wave skips the Riccati sweep.
+        auto adjoint_dist = [&]() {
+            double lamr;
+            {
+                const double eb = lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0;   // x_N - r_{N-1}
+                lamr = Qr * (sD[N * NX + rx] + eb);
+                lmax = fmax(lmax, fabs(lamr));
+            }
+            const double Rmr = lu ? w[NX + NU + ru] : 0.0;   // Rm of this lane's u row
+            const double upr = p.u_prev[ii * NU + ru];
+            double unx = 0.0;                                  // u_{k+1}[ru]
+            // stage operands (loaded one stage ahead): column r of A's a-rows, column ru of hFu, u_k[ru],
+            // u_{k-1}[ru], Q (d_k + x_k - r_{k-1})[r]
+            double nacol[NA], nhfu[NA], nuk, num, nqe;
+            auto load = [&](int k) {
+                load_acol(k, nacol);
+#pragma unroll
+                for (int s2 = 0; s2 < NA; ++s2) nhfu[s2] = sFu[k * FU + s2 * NU + ru];
+                nuk = sU[k * NU + ru];
+                const double ump = sU[(k > 0 ? k - 1 : 0) * NU + ru];
+                num = k == 0 ? upr : ump;
+                const int km = k > 0 ? k - 1 : 0;
+                const double xk = sX[k * NX + rx], trm = tr[km * NX + rx], dk = sD[k * NX + rx];
+                nqe = Qr * (dk + (xk - trm));
+            };
+            load(N - 1);
+#pragma unroll 2
+            for (int k = N - 1; k >= 0; --k) {
+                double acol[NA], hfu[NA];
+#pragma unroll
+                for (int s2 = 0; s2 < NA; ++s2) {
+                    acol[s2] = nacol[s2];
+                    hfu[s2] = nhfu[s2];
+                }
+                const double uk = nuk, um = num, qe = nqe;
+                load(k > 0 ? k - 1 : 0);
+                double lamb[NX];
+                sfor<0, NX>([&](auto I) { lamb[I] = row_bcast<I>(lamr); });
+                double g = 0.0;
+#pragma unroll
+                for (int s2 = 0; s2 < NA; ++s2) g = fma(hfu[s2], lamb[NQ + s2], g);
+                g = fma(Rr, uk - um, fma(Rmr, uk, g));
+                if (k + 1 < N) g -= Rr * (unx - uk);
+                unx = uk;
+                if (lu) {
+                    gmax = fmax(gmax, fabs(2.0 * g));
+                    nonfinite |= !isfinite(g);
+                }
+                if (k >= 1) {   // (A^T lam)[r] + Q e_{k-1}[r], two partial sums
+                    double t0 = lx ? lamr + qe : 0.0, t1 = 0.0;
+#pragma unroll
+                    for (int z = 0; z < NQ; ++z) t1 = fma(hq[z], lamb[z], t1);
+#pragma unroll
+                    for (int s2 = 0; s2 < NA; ++s2) {
+                        if (s2 & 1) t1 = fma(acol[s2], lamb[NQ + s2], t1);
+                        else t0 = fma(acol[s2], lamb[NQ + s2], t0);
+                    }
+                    lamr = lx ? t0 + t1 : 0.0;
+                    lmax = fmax(lmax, fabs(lamr));
+                }
+            }
+        };
+        auto backward_dist = [&]() {
+            double Prow[NS], pvr;
+#pragma unroll
+            for (int j = 0; j < NS; ++j) Prow[j] = j < NX ? qoh[j] : 0.0;   // P~_N = blkdiag(Q, 0)
+            pvr = Qr * (lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0);   // Q (x_N - r_{N-1})
+            // (the sweep is issue-bound: its LDS operands are read in place; a prefetch buffer spills to AGPRs)
+            for (int k = N - 1; k >= 0; --k) {
+                double hFq[SQ], hFqd[FD], hFu[FU], cc[NX], u[NU], um[NU], acol[NA];
+#pragma unroll
+                for (int i = 0; i < FQ; ++i) hFq[i] = sFq[k * FQ + i];
+#pragma unroll
+                for (int i = 0; i < FD; ++i) hFqd[i] = sFqd[k * FD + i];
+#pragma unroll
+                for (int i = 0; i < FU; ++i) hFu[i] = sFu[k * FU + i];
+#pragma unroll
+                for (int q = 0; q < NX; ++q) cc[q] = sC[k * NX + q];
+                const int km = k >= 1 ? k - 1 : 0;
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    u[c] = sU[k * NU + c];
+                    const double v = sU[km * NU + c];
+                    um[c] = (k == 0) ? up[c] : v;
+                }
+                load_acol(k, acol);
+                const double xk = sX[k * NX + rx], trm = tr[km * NX + rx];
+                const double exr = lx ? xk - trm : 0.0;
+                const double duu = sU[k * NU + ru] - sU[km * NU + ru];
+                // T = P~ [B; I] (row r), mv = P~_x. c + p~ (row r)
+                double T[NU], mv = pvr;
+#pragma unroll
+                for (int b = 0; b < NU; ++b) {
+                    double t = Prow[NX + b];
+#pragma unroll
+                    for (int s2 = 0; s2 < NA; ++s2) t = fma(Prow[NQ + s2], hFu[s2 * NU + b], t);
+                    T[b] = t;
+                }
+#pragma unroll
+                for (int q = 0; q < NX; ++q) mv = fma(Prow[q], cc[q], mv);
+                double Tb[NS][NU], mvb[NS];
+                sfor<0, NS>([&](auto I) {
+#pragma unroll
+                    for (int b = 0; b < NU; ++b) Tb[I][b] = row_bcast<I>(T[b]);
+                    mvb[I] = row_bcast<I>(mv);
+                });
+                // H_ww = B^T P_xx B + B^T P_xu + P_ux B + P_uu + R + Rm, h_w (redundant)
+                double Hww[NU][NU], hw[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+#pragma unroll
+                    for (int b = a; b < NU; ++b) {
+                        double t = Tb[NX + a][b];
+#pragma unroll
+                        for (int s2 = 0; s2 < NA; ++s2) t = fma(hFu[s2 * NU + a], Tb[NQ + s2][b], t);
+                        if (a == b) t += R[a] + Rm[a];
+                        Hww[a][b] = t;
+                        Hww[b][a] = t;
+                    }
+                    double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], mvb[NX + a]));
+#pragma unroll
+                    for (int s2 = 0; s2 < NA; ++s2) t = fma(hFu[s2 * NU + a], mvb[NQ + s2], t);
+                    hw[a] = t;
+                }
+                // column r of Y = [H_wx | -R | .]: x-lanes (A^T T)[r], u-lanes -R e_{r-NX}
+                double Ycol[NU];
+#pragma unroll
+                for (int a = 0; a < NU; ++a) {
+                    double tb[NX];
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) tb[q] = Tb[q][a];
+                    Ycol[a] = colA(T[a], acol, tb) - rdg[a];
+                }
+                // Kcol = H_ww^-1 Ycol (this lane's column of K~), kff = H_ww^-1 h_w (redundant)
+                double Kcol[NU], kff[NU], Ku[NU][NU];
+                if constexpr (NU == 2) {
+                    const double det = fma(Hww[0][0], Hww[1][1], -Hww[0][1] * Hww[0][1]);
+                    fact_ok &= (Hww[0][0] > 0.0) && (det > 0.0) && isfinite(det);
+                    const double idet = rcp_nr(det);
+                    const double i00 = Hww[1][1] * idet, i11 = Hww[0][0] * idet, i01 = -Hww[0][1] * idet;
+                    Kcol[0] = fma(i00, Ycol[0], i01 * Ycol[1]);
+                    Kcol[1] = fma(i01, Ycol[0], i11 * Ycol[1]);
+                    kff[0] = fma(i00, hw[0], i01 * hw[1]);
+                    kff[1] = fma(i01, hw[0], i11 * hw[1]);
+                    Ku[0][0] = -i00 * R[0];
+                    Ku[0][1] = -i01 * R[1];
+                    Ku[1][0] = -i01 * R[0];
+                    Ku[1][1] = -i11 * R[1];
+                } else {   // Cholesky H_ww = L L^T (rsq + Newton), solves with L and L^T
+                    double Ld[NU][NU], il[NU];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        double sd = Hww[a][a];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) sd = fma(-Ld[a][q], Ld[a][q], sd);
+                        fact_ok &= (sd > 0.0) && isfinite(sd);
+                        const double sp = fmax(sd, 1e-300);
+                        double rr = __builtin_amdgcn_rsq(sp);
+                        rr = rr * fma(-0.5 * sp * rr, rr, 1.5);
+                        rr = rr * fma(-0.5 * sp * rr, rr, 1.5);
+                        Ld[a][a] = sp * rr;
+                        il[a] = rr;
+#pragma unroll
+                        for (int b = a + 1; b < NU; ++b) {
+                            double t = Hww[a][b];
+#pragma unroll
+                            for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
+                            Ld[b][a] = t * il[a];
+                        }
+                    }
+                    auto chol_solve = [&](const double* rhs, double* out) {
+                        double y[NU];
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) {
+                            double t = rhs[a];
+#pragma unroll
+                            for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], y[q], t);
+                            y[a] = t * il[a];
+                        }
+#pragma unroll
+                        for (int a = NU - 1; a >= 0; --a) {
+                            double t = y[a];
+#pragma unroll
+                            for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], out[q], t);
+                            out[a] = t * il[a];
+                        }
+                    };
+                    chol_solve(Ycol, Kcol);
+                    chol_solve(hw, kff);
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) {   // column NX + c of K~: H_ww^-1 (-R_c e_c)
+                        double e[NU], o[NU];
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) e[a] = (a == c) ? -R[c] : 0.0;
+                        chol_solve(e, o);
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) Ku[a][c] = o[a];
+                    }
+                }
+                // [K_k | kff_k] = -[K~ | kff~] (lane j < NS stores column j, lane NS the feed-forward column)
+                if (r <= NS) {
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) wK[(k * NU + a) * (NS + 1) + r] = -(r < NS ? Kcol[a] : kff[a]);
+                }
+                if (k == 0) break;
+                // A^T P_xx A (row r) from the broadcast P_xx, p~_x = A^T mv + Q (x_k - r_{k-1})
+                double Pb[NX][NX];
+                sfor<0, NX>([&](auto I) {
+#pragma unroll
+                    for (int j = I; j < NX; ++j) {
+                        Pb[I][j] = row_bcast<I>(Prow[j]);
+                        Pb[j][I] = Pb[I][j];
+                    }
+                });
+                double Ur[NX], Pn[NX];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) {
+                    double pc[NX];
+#pragma unroll
+                    for (int q = 0; q < NX; ++q) pc[q] = Pb[q][j];
+                    Ur[j] = colA(Prow[j], acol, pc);
+                }
+                at_mul<NQ, NA, double>(h, hFq, hFqd, Ur, Pn);
+                double pn = colA(mv, acol, mvb);
+                pn = lx ? fma(Qr, exr, pn) : (lu ? -Rr * duu : 0.0);
+                // K~ columns of the other lanes
+                double Kb[NU][NX];
+                sfor<0, NX>([&](auto I) {
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) Kb[a][I] = row_bcast<I>(Kcol[a]);
+                });
+                // P~_k = blkdiag(A^T P_xx A + Q, R) - Y^T K~, p~_k = pn - Y^T kff (row r)
+#pragma unroll
+                for (int j = 0; j < NS; ++j) {
+                    double v = j < NX ? Pn[j] + qoh[j] : rdg[j - NX];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) v = fma(-Ycol[a], j < NX ? Kb[a][j] : Ku[a][j - NX], v);
+                    Prow[j] = v;
+                }
+                double pv2 = pn;
+#pragma unroll
+                for (int a = 0; a < NU; ++a) pv2 = fma(-Ycol[a], kff[a], pv2);
+                pvr = pv2;
+            }
+        };
+        if constexpr (DIST) {
+            d_recursion_dist();
+            adjoint_dist();
+            lmax = group_max(lmax);
+            gmax = group_max(gmax);
+        } else if (gl == 0) {
             {
                 double d[NX];
 #pragma unroll
@@ -707,9 +1076,11 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             }
             backward(0);
         }
-        gmax = group_bcast(gmax, gbase);
-        lmax = group_bcast(lmax, gbase);
-        fact_ok = group_bcast_i(fact_ok, gbase);
+        if constexpr (!DIST) {
+            gmax = group_bcast(gmax, gbase);
+            lmax = group_bcast(lmax, gbase);
+            fact_ok = group_bcast_i(fact_ok, gbase);
+        }
         MMPC_PHASE(2);
         nonfinite = (group_max((double)nonfinite) != 0.0);
         kkt = fmax(gmax, cmax);
@@ -734,6 +1105,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             status = ST_MAX_ITER;
             break;
         }
+        MMPC_PHASE(9);
+        if constexpr (DIST) backward_dist();   // Riccati sweep (fact_ok is uniform over the group)
         if (!fact_ok) {
             status = ST_FACT_FAILED;
             break;
@@ -745,21 +1118,93 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                                     : mub;
 
         MMPC_PHASE(3);
-        if (gl == 0) {
-            for (int pass = 0;; ++pass) {
-                if (pass > 0) backward(pass);
-                if (!fact_ok) break;
-                resolve = false;
-                step_sweep(pass);
-                if (!BOUNDED || !resolve || pass + 1 >= kBoundPasses) break;
+        if constexpr (DIST) {
+            // step sweep: lane r holds s_k[r], s = [dx_k; du_{k-1}]; u-lanes du_k = K_k s_k + kff_k (row r - NX of
+            // K from the workspace), x-lanes dx_{k+1} = A dx + B du + c.  A dx_k + B du_k goes to sD[k+1] (d is
+            // dead after the backward sweep) for the directional derivative below.
+            if (fact_ok) {
+                double sr = 0.0;
+                if (lx) sDX[rx] = 0.0;
+                constexpr int NK = NS + 1;
+                const double* const Kp = wK + ru * NK;   // row ru of K_k | kff_k at Kp + k NU NK
+                // operands double-buffered two stages ahead (manual unroll by two, so the buffers are renamed, not
+                // copied): the K row from the HBM/L2 workspace, row r of [A - I | B] and c_k[r] from LDS
+                struct Ops {
+                    double K[NK], a[NX], b[NU], c;
+                };
+                auto fetch = [&](int k, Ops& o) {
+#pragma unroll
+                    for (int j = 0; j < NK; ++j) o.K[j] = Kp[k * NU * NK + j];
+                    load_arow(k, o.a, o.b);
+                    o.c = sC[k * NX + rx];
+                };
+                auto stage = [&](int k, Ops& o) {
+                    double sb[NS];
+                    sfor<0, NS>([&](auto I) { sb[I] = row_bcast<I>(sr); });
+                    double du0 = o.K[NS], du1 = 0.0;
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) {
+                        if (j & 1) du1 = fma(o.K[j], sb[j], du1);
+                        else du0 = fma(o.K[j], sb[j], du0);
+                    }
+                    const double du = du0 + du1;
+                    double ad = sr;
+#pragma unroll
+                    for (int j = 0; j < NX; ++j) ad = fma(o.a[j], sb[j], ad);
+                    double dub[NU];
+                    sfor<0, NU>([&](auto I) { dub[I] = row_bcast<NX + I>(du); });
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) ad = fma(o.b[c], dub[c], ad);
+                    const double dxn = ad + o.c;
+                    if (lx) {
+                        sDX[(k + 1) * NX + rx] = dxn;
+                        sD[(k + 1) * NX + rx] = ad;
+                    }
+                    if (lu) sDU[k * NU + ru] = du;
+                    sr = lx ? dxn : (lu ? du : 0.0);
+                    fetch(k + 2 < N ? k + 2 : N - 1, o);   // unconditional: static wait counts
+                };
+                Ops o0, o1;
+                fetch(0, o0);
+                if (N > 1) fetch(1, o1);
+                for (int k = 0; k < N; k += 2) {
+                    stage(k, o0);
+                    if (k + 1 < N) stage(k + 1, o1);
+                }
             }
+            __builtin_amdgcn_wave_barrier();
+            // directional derivative of J along (dx, du), stage-parallel:
+            // sum_k 2Q(F_k - r_k).(A dx_k + B du_k) + 2R(u_k - u_{k-1})(du_k - du_{k-1}) + 2Rm u_k du_k
+            double dj = 0.0;
+            for (int k = gl; k < N; k += G) {
+#pragma unroll
+                for (int q = 0; q < NX; ++q) dj = fma(2.0 * Q[q] * (sF[k * NX + q] - tr[k * NX + q]), sD[(k + 1) * NX + q], dj);
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    const double uk = sU[k * NU + c], duk = sDU[k * NU + c];
+                    const double um = (k == 0) ? up[c] : sU[(k - 1) * NU + c];
+                    const double dum = (k == 0) ? 0.0 : sDU[(k - 1) * NU + c];
+                    dj = fma(2.0 * R[c] * (uk - um), duk - dum, fma(2.0 * Rm[c] * uk, duk, dj));
+                }
+            }
+            dJ = group_sum(dj);
+        } else {
+            if (gl == 0) {
+                for (int pass = 0;; ++pass) {
+                    if (pass > 0) backward(pass);
+                    if (!fact_ok) break;
+                    resolve = false;
+                    step_sweep(pass);
+                    if (!BOUNDED || !resolve || pass + 1 >= kBoundPasses) break;
+                }
+            }
+            fact_ok = group_bcast_i(fact_ok, gbase);
+            dJ = group_bcast(dJ, gbase);
         }
-        fact_ok = group_bcast_i(fact_ok, gbase);
         if (!fact_ok) {
             status = ST_FACT_FAILED;
             break;
         }
-        dJ = group_bcast(dJ, gbase);
         __builtin_amdgcn_wave_barrier();
         MMPC_PHASE(4);
         // interior point: fraction to the boundary (primal alpha_max, dual alpha_z), barrier directional derivative

@@ -1,0 +1,46 @@
+"""bench.py's multi-GPU launcher on CPU (gloo, stand-in solver): ``--gpus N`` without WORLD_SIZE starts N rank
+processes, each solves its own shard of global instances [r B, (r+1) B), the per-step results reach rank 0's
+host through one all_gather_into_tensor, and the JSON line reports the whole job (n_gpus = N,
+global_batch = N B).  The stand-in solver is bench.py's plumbing double, not the solve path (no GPU here)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+
+def _run(*args, env_extra=None):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("gpus", [1, 2, 3])
+def test_launcher_spawns_ranks(gpus):
+    B = 8
+    out = _run("--standin", "--gpus", str(gpus), "--batch", str(B), "--steps", "3", "--warmup", "1",
+               "--no-cpu-baseline")
+    assert out["n_gpus"] == gpus
+    assert out["config"]["global_batch"] == gpus * B and out["config"]["batch_per_gpu"] == B
+    assert out["gathered_results_match"] is True
+    assert out["converged"] == gpus * B
+    assert out["steps"] == 3 and out["warmup"] == 1 and out["scaling"] == "weak"
+    # rank r's rows are global instances r*B .. r*B+B-1 (u_0* := x0[:, 0] = global index in the stand-in)
+    assert out["standin_u0_first_col"] == [float(i) for i in range(gpus * B)]
+    assert out["value"] > 0 and out["ms_per_step"] > 0
+
+
+def test_launcher_propagates_rank_failure():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--standin", "--gpus", "2",
+                        "--config", "nope"], capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode != 0

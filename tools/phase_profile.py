@@ -35,8 +35,8 @@ L = mmpc.lib()
 L.mmpc_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
 path = mmpc.write_model_json("/tmp/mmpc_phase.json", "phase", nx, nu, 2000, N)
 s = mmpc.Solver(path, kkt_solver=a.kkt)
-NAMES_GROUP = ["load", "A:evals(parallel)", "B:d+backward(serial)", "check", "C:step(serial)", "D:line_search",
-               "update+after_loop", "writeback", "-", "-"]
+NAMES_GROUP = ["load", "A:evals(parallel)", "B:d+adjoint(+riccati if not DIST)", "riccati(DIST)+mu",
+               "C:step(serial)+dJ", "D:line_search", "after_loop", "writeback", "update(loop top)", "check"]
 if a.kkt == 3:
     NAMES = NAMES_GROUP
 elif exo or a.kkt == 2 or N * nu > 64:
