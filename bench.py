@@ -375,17 +375,20 @@ def roofline(args, cfg, mmpc, ksolver, N, nx, nu, B, iters, kern_ms):
     own = float(iters.sum()) * fl["total"] / sec / 1e12
     survey = float(iters.sum()) * mmpc.survey_flops_per_iteration(N, nx, nu) / sec / 1e12
     traffic = None
-    key = f"{args.config}:{kname}"
-    if os.path.exists(args.traffic_json):
+    traffic_src, pmc = None, {}
+    if os.path.exists(args.traffic_json):   # keyed "<config>:<kernel name prefix>"
         try:
-            tj = json.load(open(args.traffic_json)).get(key, {})
-            if tj.get("batch") == B and tj.get("horizon") == N:
-                traffic = tj.get("hbm_bytes_per_launch")
+            for key, tj in json.load(open(args.traffic_json)).items():
+                if (key.startswith(f"{args.config}:{kname}") and isinstance(tj, dict) and tj.get("batch") == B
+                        and tj.get("horizon") == N and tj.get("kernel_ms_at_measurement") is not None
+                        and abs(tj["kernel_ms_at_measurement"] - kern_ms) <= 0.25 * kern_ms):
+                    traffic, traffic_src, pmc = tj.get("hbm_bytes_per_launch"), tj.get("source"), tj
         except (OSError, ValueError):
             traffic = None
     alg_bytes = B * (8 * (nx + nu + N * nx + 2 * (nx * (N + 1) + nu * N)) + 12)   # SURVEY.md 8d, per launch
     return {"bound": "fp64-valu", "achieved": own, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": own / FP64_PEAK_TFLOPS, "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": kname,
             "flops_per_iter_kernel_own_count": fl["total"],
             "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N, nx, nu),
@@ -393,8 +396,13 @@ def roofline(args, cfg, mmpc, ksolver, N, nx, nu, B, iters, kern_ms):
             "survey_8d_equivalent_frac": survey / FP64_PEAK_TFLOPS,
             "algorithmic_hbm_bytes_per_launch": alg_bytes,
             "hbm_gbs_algorithmic": alg_bytes / sec / 1e9,
-            "mfma_instructions": 0,
-            "note": "frac = kernel's own flops / FP64 vector peak; MFMA/FP64-VALU counters: profiles/r02/"}
+            "pmc_fp64_valu_flops_issued_per_launch": pmc.get("fp64_valu_flops_issued_per_launch"),
+            "pmc_fp64_valu_frac_issued": (pmc["fp64_valu_flops_issued_per_launch"] / sec / 1e12 / FP64_PEAK_TFLOPS
+                                          if pmc.get("fp64_valu_flops_issued_per_launch") else None),
+            "pmc_mfma_counters": pmc.get("mfma_counters"),
+            "note": "frac = the kernel's own algorithmic flops / FP64 vector peak (no kernel issues MFMA: DESIGN.md "
+                    "'Why no MFMA'); pmc_* = rocprofv3 counters of the same kernel (tools/pmc.sh) when they match "
+                    "this run's shape and kernel time: issued FP64 VALU lane-flops incl. inactive-lane slots"}
 
 
 def main():

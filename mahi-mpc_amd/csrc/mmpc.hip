@@ -71,13 +71,10 @@ struct mmpc_handle {
     double* ws = nullptr;
     size_t ws_bytes = 0;
     int ws_dev = -1;
-    // state bounds of x_1..x_N (JSON x_min/x_max, or mmpc_set_state_bounds); a device copy for the kernels
+    // state bounds of x_1..x_N (JSON x_min/x_max, or mmpc_set_state_bounds); copied into each launch's arguments
     double x_lb[16], x_ub[16];
     bool x_bounded = false;
     std::mutex xb_mu;
-    double* d_xb = nullptr;  // [2][nx]
-    int d_xb_dev = -1;
-    bool d_xb_dirty = true;
 };
 
 namespace {
@@ -507,8 +504,9 @@ int set_dynamic_lds(K kernel, size_t bytes) {
 int resolve_kkt_solver_base(const mmpc_handle* h, int64_t B);
 int resolve_kkt_solver(const mmpc_handle* h, int64_t B) {
     const int s = resolve_kkt_solver_base(h, B);
-    // state bounds (interior-point variant): the Riccati solvers only
-    if (h->x_bounded && h->opts.kkt_solver == MMPC_KKT_AUTO && s == MMPC_KKT_CONDENSED) return MMPC_KKT_RICCATI_GROUP;
+    // state bounds (interior-point variant): the Riccati solvers only; the group kernel when its LDS layout fits
+    if (h->x_bounded && h->opts.kkt_solver == MMPC_KKT_AUTO && s == MMPC_KKT_CONDENSED)
+        return group_lds_bytes(h->info, h->nq, true, true) <= kMaxGroupLds ? MMPC_KKT_RICCATI_GROUP : MMPC_KKT_RICCATI;
     return s;
 }
 int resolve_kkt_solver_base(const mmpc_handle* h, int64_t B) {
@@ -519,7 +517,9 @@ int resolve_kkt_solver_base(const mmpc_handle* h, int64_t B) {
     // (B <= 2560 at N*nu <= 64), the 16-lane Riccati kernel up to B*N = 1e6, one lane per instance beyond;
     // exo -- the 16-lane kernel while at least two of its workgroups fit a CU's LDS and B <= 4096
     const int N = mi.num_shooting_nodes;
-    const size_t glds = group_lds_bytes(mi, h->nq, true);  // with the bounded solves' hold targets (larger)
+    // LDS of the layout launch_kernel will use: the interior-point fields with state bounds, else the bounded
+    // solves' hold targets (the larger of the two control-bound variants)
+    const size_t glds = group_lds_bytes(mi, h->nq, true, h->x_bounded);
     if (mi.model_id == MMPC_MODEL_USER) {  // SX-generated dynamics: no condensed kernel (it is 2-link specific)
         if (glds <= kMaxGroupLds / 2 && B * static_cast<int64_t>(N) <= 1000000) return MMPC_KKT_RICCATI_GROUP;
         return MMPC_KKT_RICCATI;
@@ -538,33 +538,6 @@ int launch_group(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const So
     int rc = set_dynamic_lds(sqp_group_kernel<Model, BOUNDED, XB>, lds);
     if (rc) return rc;
     sqp_group_kernel<Model, BOUNDED, XB><<<grid, block, lds, stream>>>(p, gwk);
-    return MMPC_OK;
-}
-
-// the state bounds on the current device (synchronous upload when they changed or the device did)
-int ensure_state_bounds_device(mmpc_handle* h, const double** lb, const double** ub) {
-    int dev = -1;
-    MMPC_HIP(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(h->xb_mu);
-    const int nx = h->info.num_x;
-    if (!h->d_xb || h->d_xb_dev != dev) {
-        if (h->d_xb) MMPC_HIP(hipFree(h->d_xb));
-        h->d_xb = nullptr;
-        MMPC_HIP(hipMalloc(reinterpret_cast<void**>(&h->d_xb), 2 * nx * sizeof(double)));
-        h->d_xb_dev = dev;
-        h->d_xb_dirty = true;
-    }
-    if (h->d_xb_dirty) {
-        double hb[32];
-        for (int i = 0; i < nx; ++i) {
-            hb[i] = h->x_lb[i];
-            hb[nx + i] = h->x_ub[i];
-        }
-        MMPC_HIP(hipMemcpy(h->d_xb, hb, 2 * nx * sizeof(double), hipMemcpyHostToDevice));
-        h->d_xb_dirty = false;
-    }
-    *lb = h->d_xb;
-    *ub = h->d_xb + nx;
     return MMPC_OK;
 }
 
@@ -634,10 +607,13 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
     // points pass NULL for bounds that are all infinite
     const bool bounded = u_lb || u_ub;
-    p.x_lb = p.x_ub = nullptr;
-    if (h->x_bounded) {  // state bounds: the interior-point variant (sqp_wave.h "state bounds")
-        int rc = ensure_state_bounds_device(h, &p.x_lb, &p.x_ub);
-        if (rc) return rc;
+    {  // state bounds: the interior-point variant (sqp_wave.h "state bounds"), by value in the launch arguments
+        std::lock_guard<std::mutex> lk(h->xb_mu);
+        p.x_bounded = h->x_bounded;
+        for (int i = 0; i < 16; ++i) {
+            p.x_lb[i] = i < mi.num_x ? h->x_lb[i] : -INFINITY;
+            p.x_ub[i] = i < mi.num_x ? h->x_ub[i] : INFINITY;
+        }
     }
     const int solver = resolve_kkt_solver(h, B);
     return launch_kernel(h, solver, p, bounded, stream);
@@ -650,7 +626,7 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
     const int N = mi.num_shooting_nodes;
     if (solver == MMPC_KKT_RICCATI_GROUP) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 needs the lane Riccati solver");
-        const bool xb = p.x_lb != nullptr;
+        const bool xb = p.x_bounded != 0;
         const size_t lds = group_lds_bytes(mi, h->nq, bounded, xb);
         if (lds > kMaxGroupLds) return fail(MMPC_ERR_UNSUPPORTED, "group Riccati solver: stage data exceeds 160 KB LDS");
         LaneWork lw;
@@ -668,7 +644,7 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         MMPC_HIP(hipGetLastError());
         return MMPC_OK;
     }
-    if (p.x_lb && solver == MMPC_KKT_CONDENSED)
+    if (p.x_bounded && solver == MMPC_KKT_CONDENSED)
         return fail(MMPC_ERR_UNSUPPORTED, "state bounds need a Riccati solver (MMPC_KKT_RICCATI[_GROUP])");
     if (solver == MMPC_KKT_CONDENSED) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 is a Riccati-solver option");
@@ -697,8 +673,8 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         const bool f32 = h->opts.factor_fp32 != 0;
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
-            if (f32) launch_lane<M, float>(bounded, p.x_lb != nullptr, grid, block, stream, p, lw);
-            else launch_lane<M, double>(bounded, p.x_lb != nullptr, grid, block, stream, p, lw);
+            if (f32) launch_lane<M, float>(bounded, p.x_bounded != 0, grid, block, stream, p, lw);
+            else launch_lane<M, double>(bounded, p.x_bounded != 0, grid, block, stream, p, lw);
             return MMPC_OK;
         });
         if (rc) return rc;
@@ -790,10 +766,6 @@ int mmpc_destroy(mmpc_handle* h) {
         DeviceGuard g(h->ws_dev);
         (void)hipFree(h->ws);
     }
-    if (h->d_xb) {
-        DeviceGuard g(h->d_xb_dev);
-        (void)hipFree(h->d_xb);
-    }
     delete h;
     return MMPC_OK;
 }
@@ -824,7 +796,6 @@ int mmpc_set_state_bounds(mmpc_handle* h, const double* x_lb, const double* x_ub
         any |= l > -1e19 || u < 1e19;
     }
     h->x_bounded = any;
-    h->d_xb_dirty = true;
     return MMPC_OK;
 }
 

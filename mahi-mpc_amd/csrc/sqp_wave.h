@@ -46,8 +46,11 @@ struct SolveParams {
     int64_t w_stride;
     const double* u_lb;
     const double* u_ub;
-    const double* x_lb;  // state bounds of x_1..x_N [nx] (ModelControl.cpp:37-50), or nullptr: interior point
-    const double* x_ub;
+    // state bounds of x_1..x_N (ModelControl.cpp:37-50) BY VALUE (nx <= 16): a solve captures the bounds of its
+    // launch, so mmpc_set_state_bounds between stream-ordered solves never changes one already in flight
+    int x_bounded;  // any finite state bound: the interior-point variant
+    double x_lb[16];
+    double x_ub[16];
     double* V;
     int32_t* status;
     int32_t* iters;
@@ -113,8 +116,8 @@ template <int NX, int NU>
 __device__ __forceinline__ void load_ip_bounds(const SolveParams& p, double* yl, double* yu) {
 #pragma unroll
     for (int j = 0; j < NX + NU; ++j) {
-        const double* lo = j < NX ? p.x_lb : p.u_lb;
-        const double* hi = j < NX ? p.x_ub : p.u_ub;
+        const double* lo = j < NX ? (p.x_bounded ? p.x_lb : nullptr) : p.u_lb;
+        const double* hi = j < NX ? (p.x_bounded ? p.x_ub : nullptr) : p.u_ub;
         const int i = j < NX ? j : j - NX;
         yl[j] = (lo && lo[i] > -1e19) ? lo[i] : -INFINITY;
         yu[j] = (hi && hi[i] < 1e19) ? hi[i] : INFINITY;

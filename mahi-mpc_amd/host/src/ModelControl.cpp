@@ -104,10 +104,17 @@ std::vector<std::vector<double>> ModelControl::calc_u_batch(const std::vector<st
         tr.insert(tr.end(), trajs[b].begin(), trajs[b].end());
     }
     const std::vector<double> w = packed_weights();
+    std::vector<double> lb, ub;
+    {
+        std::lock_guard<std::mutex> lg(m_control_limits_mutex);  // the limits calc_u enforces (ModelControl.cpp:148-154)
+        lb = model_parameters.u_min;
+        ub = model_parameters.u_max;
+    }
     std::vector<int32_t> st(B, -1), it(B, 0);
     std::vector<double> kkt(B, 0.0);
     m_backend->check(m_backend->solve_batch_host(m_handle, static_cast<int64_t>(B), x0.data(), up.data(), tr.data(), w.data(), 0,
-                                nullptr, nullptr, V.data(), st.data(), it.data(), kkt.data()),
+                                lb.size() == nu ? lb.data() : nullptr, ub.size() == nu ? ub.data() : nullptr,
+                                V.data(), st.data(), it.data(), kkt.data()),
           "mmpc_solve_batch_host");
     std::vector<std::vector<double>> out(B);
     for (size_t b = 0; b < B; ++b) out[b].assign(V.begin() + b * m_V.size(), V.begin() + (b + 1) * m_V.size());

@@ -113,3 +113,26 @@ def test_generated_linear_functions_casadi_abi(golden_kat, oracle, mmpc_mod, tmp
             np.testing.assert_array_equal(xd, xdd[0])
             np.testing.assert_allclose(A, Aref, rtol=tol, atol=tol * np.abs(Aref).max())
             np.testing.assert_allclose(Bm, Bref, rtol=tol, atol=tol * np.abs(Bref).max())
+
+
+def test_calc_u_batch_enforces_control_limits(oracle, tmp_path):
+    """ModelControl::calc_u_batch with update_control_limits (ModelControl.cpp:148-154,205-209): the batched
+    solutions stay inside the control box and equal the oracle's bounded GN-SQP (same KKT point; 1e-9)."""
+    subprocess.run(["make", "-s", "-C", HOST], check=True)
+    N, B, lim = 30, 24, 2.0
+    x0, up, tr = oracle.synth(20250213, 0, B, N, 0.002)
+    stdin = "\n".join(" ".join(repr(float(v)) for v in np.concatenate([x0[b], up[b], tr[b].ravel()]))
+                      for b in range(B))
+    out = subprocess.run([os.path.join(HOST, "bin", "calc_u_batch_example"), str(N), str(lim)], cwd=tmp_path,
+                         input=stdin, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    rows = np.array([[float(v) for v in line.split()] for line in out.stdout.splitlines()
+                     if line[:1].isdigit() or line[:1] == "-"])   # ModelGenerator prints progress lines first
+    assert rows.shape == (B, 1 + 4 * (N + 1) + 2 * N)
+    st, V = rows[:, 0].astype(int), rows[:, 1:]
+    assert (st == 0).all(), st
+    U = np.stack([V[:, 6 * k + 4:6 * k + 6] for k in range(N)], axis=1)
+    assert (np.abs(U) <= lim).all()
+    assert (np.abs(U) == lim).any()   # the limits bind for some of these instances
+    o = oracle.solve_batch(N, 0.002, x0, up, tr, np.array(WEIGHTS_CFG), u_lb=[-lim, -lim], u_ub=[lim, lim])
+    np.testing.assert_allclose(V, o["V"], rtol=0, atol=1e-9 * np.abs(o["V"]).max())

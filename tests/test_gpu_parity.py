@@ -2,12 +2,13 @@
 fixtures, plus size-independent properties at the full cfg#2 size (B = 4096).
 
 Tolerances (stated per test):
-  * GPU vs oracle, same algorithm: V* within 1e-9 relative to max|V| and identical iteration counts
+  * GPU vs oracle, same algorithm: V* within 1e-10 relative to max|V| and identical iteration counts
     for >= 99 % of instances; where the counts differ (a stop test landing on either side of its
     threshold after roundoff) within the solution accuracy the stop test guarantees, 1e-6.
   * GPU vs scipy golden (independent solver): V* within 1e-6 relative, J* within 1e-8 relative.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -36,13 +37,20 @@ def _rel(a, b):
     return np.abs(a - b).max(1) / np.maximum(np.abs(b).max(1), 1e-300)
 
 
-def _compare(gpu, orc, tol_same=1e-9, tol_diff=1e-6, min_same=0.99, dump=None):
+def _compare(gpu, orc, tol_same=1e-10, tol_diff=1e-6, min_same=0.99, dump=None):
     """Same algorithm on both sides: identical iteration counts except where a stop test lands within
-    roundoff of its threshold (allowed for max(2, 1 %) of the instances); V* within tol_same where the
-    counts agree and within the stop test's accuracy (tol_diff) where they differ."""
+    roundoff of its threshold (allowed for max(2, 1 %) of the instances); V* within tol_same (SURVEY.md A9:
+    1e-10 relative, same algorithm) where the counts agree and within the stop test's accuracy (tol_diff)
+    where they differ.  MMPC_TEST_DUMP=1 saves the inputs of status mismatches under gpurun_out/."""
     same = gpu["iters"] == orc["iters"]
     bad_status = gpu["status"] != orc["status"]
-    if dump is not None and bad_status.any():
+    if os.environ.get("MMPC_TEST_LOG"):   # diagnostics: the achieved agreement of every comparison
+        with open(os.environ["MMPC_TEST_LOG"], "a") as f:
+            r = _rel(gpu["V"], orc["V"])
+            f.write(f"{os.environ.get('PYTEST_CURRENT_TEST', '?')} n={len(same)} same={int(same.sum())} "
+                    f"max_rel_same={r[same].max() if same.any() else 0:.3e} max_rel={r.max():.3e}\n")
+    if dump is not None and bad_status.any() and os.environ.get("MMPC_TEST_DUMP"):
+        os.makedirs(os.path.dirname(dump), exist_ok=True)
         np.savez(dump, idx=np.where(bad_status)[0], gpu_status=gpu["status"][bad_status],
                  orc_status=orc["status"][bad_status], gpu_iters=gpu["iters"][bad_status],
                  orc_iters=orc["iters"][bad_status], **{k: v[bad_status] for k, v in dump_inputs.items()})
@@ -136,8 +144,7 @@ def test_cfg2_full_batch_vs_oracle(model_json, mmpc_mod, oracle, torch_cuda):
     xo, uo, to = x0.cpu().numpy(), up.cpu().numpy(), tr.cpu().numpy()
     orc = oracle.solve_batch(N, H, xo, uo, to, np.array(WEIGHTS_CFG))
     nc = np.where((gpu["status"] != 0) | (orc["status"] != 0))[0]
-    if len(nc):
-        import os
+    if len(nc) and os.environ.get("MMPC_TEST_DUMP"):
         os.makedirs("gpurun_out", exist_ok=True)
         np.savez("gpurun_out/cfg2_nonconverged.npz", idx=nc, x0=xo[nc], u_prev=uo[nc], traj=to[nc],
                  gpu_status=gpu["status"][nc], gpu_iters=gpu["iters"][nc], gpu_kkt=gpu["kkt"][nc],
@@ -146,8 +153,6 @@ def test_cfg2_full_batch_vs_oracle(model_json, mmpc_mod, oracle, torch_cuda):
                                          int(orc["status"][i]), int(orc["iters"][i]), float(orc["kkt"][i])) for i in nc]
     assert (gpu["kkt"] <= 1e-8).all()
     dump_inputs.update(x0=xo, u_prev=uo, traj=to)
-    import os
-    os.makedirs("gpurun_out", exist_ok=True)
     _compare(gpu, orc, dump="gpurun_out/cfg2_status_mismatch.npz")
     dump_inputs.clear()
     # size-independent properties on every instance: pinned x_0, zero defects, stationarity
