@@ -79,6 +79,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--init", choices=["as_given", "hold_x0"], default="as_given",
                     help="mmpc_opts.init_states: the reference's cold start (V = 0) or x_1..x_N = x_0 (DESIGN 3d)")
+    ap.add_argument("--hessian", choices=["auto", "gauss_newton", "exact"], default="auto",
+                    help="mmpc_opts.hessian: AUTO = exact Lagrangian Hessian where supported (DESIGN.md 3e)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch per config (tools/pmc.sh + tools/pmc_summary.py)")
     ap.add_argument("--standin", action="store_true",
@@ -208,6 +210,7 @@ def run_rank(args):
         dev = torch.device("cpu")
         solver = _StandInSolver(nx, nu, N)
         ksolver = 0
+        hess = 1
         stream = None
     else:
         import mmpc
@@ -219,9 +222,12 @@ def run_rank(args):
         ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt]
         solver = mmpc.Solver(path, device=local, kkt_solver=ksolver, factor_fp32=cfg["fp32"],
                              tol_grad=tol_grad, tol_defect=tol_defect,
-                             init_states=mmpc.INIT_HOLD_X0 if args.init == "hold_x0" else mmpc.INIT_AS_GIVEN)
+                             init_states=mmpc.INIT_HOLD_X0 if args.init == "hold_x0" else mmpc.INIT_AS_GIVEN,
+                             hessian={"auto": mmpc.HESSIAN_AUTO, "gauss_newton": mmpc.HESSIAN_GAUSS_NEWTON,
+                                      "exact": mmpc.HESSIAN_EXACT}[args.hessian])
         solver.reserve_workspace(B)
         ksolver = solver.kkt_solver_for(B)   # the AUTO choice, resolved by the library
+        hess = solver.hessian_for(B)
         stream = torch.cuda.current_stream(dev)
     NV = solver.NV
     f64 = dict(dtype=torch.float64, device=dev)
@@ -321,6 +327,7 @@ def run_rank(args):
                    "horizon": N, "tol_grad": tol_grad, "tol_defect": tol_defect,
                    "kkt_solver": {0: "stand-in (test)", 1: "condensed (wave per instance)",
                                   2: "riccati (lane per instance)", 3: "riccati (16 lanes per instance)"}[ksolver],
+                   "hessian": {1: "gauss-newton", 2: "exact (Lagrangian, IPOPT's default)"}[hess],
                    "init_states": "V as given (reference cold start V = 0)" if args.init == "as_given"
                    else "x_1..x_N = x_0 (MMPC_INIT_HOLD_X0)",
                    "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) gathered to "

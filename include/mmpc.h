@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MMPC_ABI_VERSION 3
+#define MMPC_ABI_VERSION 4
 
 typedef struct mmpc_handle mmpc_handle;
 
@@ -114,6 +114,22 @@ enum mmpc_init_states {
                                state trajectory for cold starts, fewer SQP iterations */
 };
 
+/* Hessian of each SQP subproblem.  The reference's IPOPT uses the exact Lagrangian Hessian by default
+ * (hessian_approximation = exact; opts at ModelControl.cpp:54-59, nlp_hess_l generated at ModelGenerator.cpp:238).
+ * Both choices converge to the same KKT point; they differ in the path and the iteration count. */
+enum mmpc_hessian {
+    MMPC_HESSIAN_AUTO = 0,         /* EXACT where supported and the model enables it by default (the built-in 2-link
+                                      arm and SX-generated models; the exo keeps Gauss-Newton, whose small-residual
+                                      fits converge in 3-5 iterations), else GAUSS_NEWTON */
+    MMPC_HESSIAN_GAUSS_NEWTON = 1, /* J_F^T Q J_F + R terms: positive semidefinite, linear convergence for large
+                                      tracking residuals */
+    MMPC_HESSIAN_EXACT = 2         /* + h sum_r lam_{k+1,r} d^2 f_r/d(x_k,u_k)^2 per stage (lam: the QP adjoint);
+                                      an iteration whose KKT matrix is not positive definite on the null space takes
+                                      the Gauss-Newton step.  Supported: unbounded, nonlinear solves of models with
+                                      second derivatives on the RICCATI_GROUP solver (nx+nu < 16); a solve outside
+                                      that returns MMPC_ERR_UNSUPPORTED */
+};
+
 typedef struct mmpc_opts {
     int32_t max_iter;   /* SQP iteration cap (reference IPOPT: 200, ModelControl.cpp:55). default 50 */
     int32_t device;     /* HIP device ordinal; -1 = the calling thread's current device. default -1 */
@@ -123,6 +139,7 @@ typedef struct mmpc_opts {
     int32_t factor_fp32; /* 1: Riccati factor/solve in fp32, residuals/merit/iterates in fp64 (SURVEY 8d
                             cfg#5; each SQP iteration refines the fp32 step). Riccati solver only. default 0 */
     int32_t init_states; /* enum mmpc_init_states. default MMPC_INIT_AS_GIVEN */
+    int32_t hessian;     /* enum mmpc_hessian. default MMPC_HESSIAN_AUTO (ABI 4) */
 } mmpc_opts;
 
 typedef struct mmpc_model_info {
@@ -163,6 +180,11 @@ int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes);
 /* The KKT solver (enum mmpc_kkt_solver) a solve of B instances runs under the handle's options:
  * opts.kkt_solver, or what MMPC_KKT_AUTO picks for this model, horizon and B. */
 int mmpc_resolve_kkt_solver(const mmpc_handle* h, int64_t B, int32_t* solver);
+
+/* The Hessian (MMPC_HESSIAN_GAUSS_NEWTON or MMPC_HESSIAN_EXACT) a solve of B instances runs under the handle's
+ * options; u_bounded = whether the solve passes control bounds (the projected solves are Gauss-Newton).
+ * MMPC_ERR_UNSUPPORTED when opts.hessian = EXACT cannot be honoured for that solve. */
+int mmpc_resolve_hessian(const mmpc_handle* h, int64_t B, int32_t u_bounded, int32_t* hessian);
 
 /* Batched SQP solve, DEVICE pointers, stream-ordered.  u_lb/u_ub: device [nu] or NULL
  * (unbounded; |bound| >= 1e19 is unbounded as in IPOPT).  Finite bounds are enforced (the lbx/ubx

@@ -198,6 +198,8 @@ int validate_opts(const mmpc_opts* o) {
     if (o->factor_fp32 != 0 && o->factor_fp32 != 1) return fail(MMPC_ERR_INVALID_ARG, "factor_fp32 must be 0 or 1");
     if (o->init_states != MMPC_INIT_AS_GIVEN && o->init_states != MMPC_INIT_HOLD_X0)
         return fail(MMPC_ERR_INVALID_ARG, "unknown init_states");
+    if (o->hessian < MMPC_HESSIAN_AUTO || o->hessian > MMPC_HESSIAN_EXACT)
+        return fail(MMPC_ERR_INVALID_ARG, "unknown hessian");
     return MMPC_OK;
 }
 
@@ -525,7 +527,10 @@ int resolve_kkt_solver_base(const mmpc_handle* h, int64_t B) {
         return MMPC_KKT_RICCATI;
     }
     if (mi.model_id == MMPC_MODEL_TWO_LINK_ARM) {
-        if (N * TwoLinkArm::NU <= 64 && B <= 2560) return MMPC_KKT_CONDENSED;
+        // the condensed kernel is Gauss-Newton only: with the exact Hessian (AUTO) the 16-lane kernel takes the
+        // small batches too (fewer SQP iterations outweigh its higher per-iteration cost)
+        if (N * TwoLinkArm::NU <= 64 && B <= 2560 && (h->opts.hessian == MMPC_HESSIAN_GAUSS_NEWTON || mi.is_linear))
+            return MMPC_KKT_CONDENSED;
         if (glds <= kMaxGroupLds && B * static_cast<int64_t>(N) <= 1000000) return MMPC_KKT_RICCATI_GROUP;
         return MMPC_KKT_RICCATI;
     }
@@ -533,11 +538,49 @@ int resolve_kkt_solver_base(const mmpc_handle* h, int64_t B) {
     return MMPC_KKT_RICCATI;
 }
 
-template <class Model, bool BOUNDED, bool XB = false>
+// Exact-Hessian support of a model / solve (mmpc_opts.hessian): second derivatives, the lane-distributed path
+// of the group kernel (nx + nu < 16, no bounds), nonlinear dynamics.  AUTO also needs the model's default
+// (kExactDefault: the exo keeps Gauss-Newton -- its small-residual fits converge in 3-5 Gauss-Newton
+// iterations and the exact Hessian did not cut them in the prototype sweep).
+template <class M>
+constexpr bool exact_capable() {
+    return HasHess<M>::value && (M::NX + M::NU < kGroupLanes);
+}
+template <class M, class = void>
+struct ExactDefault {
+    static constexpr bool value = true;
+};
+template <class M>
+struct ExactDefault<M, std::enable_if_t<!M::kExactDefault || M::kExactDefault>> {
+    static constexpr bool value = M::kExactDefault;
+};
+// MMPC_HESSIAN_GAUSS_NEWTON / _EXACT for a solve under solver with/without control bounds; <0 = error
+int resolve_hessian(const mmpc_handle* h, int solver, bool u_bounded) {
+    const int want = h->opts.hessian;
+    if (want == MMPC_HESSIAN_GAUSS_NEWTON) return MMPC_HESSIAN_GAUSS_NEWTON;
+    bool capable = false, dflt = false;
+    with_model(h->info.model_id, [&](auto* m) {
+        using M = std::remove_pointer_t<decltype(m)>;
+        capable = exact_capable<M>();
+        dflt = ExactDefault<M>::value;
+        return MMPC_OK;
+    });
+    const bool ok = capable && solver == MMPC_KKT_RICCATI_GROUP && !u_bounded && !h->x_bounded &&
+                    !h->info.is_linear && !h->opts.factor_fp32;
+    if (want == MMPC_HESSIAN_EXACT) {
+        if (!ok)
+            return fail(MMPC_ERR_UNSUPPORTED, "exact Hessian: needs a model with second derivatives, the "
+                                              "RICCATI_GROUP solver and an unbounded nonlinear solve");
+        return MMPC_HESSIAN_EXACT;
+    }
+    return ok && dflt ? MMPC_HESSIAN_EXACT : MMPC_HESSIAN_GAUSS_NEWTON;
+}
+
+template <class Model, bool BOUNDED, bool XB = false, bool EXACT = false>
 int launch_group(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const SolveParams& p, GroupWork gwk) {
-    int rc = set_dynamic_lds(sqp_group_kernel<Model, BOUNDED, XB>, lds);
+    int rc = set_dynamic_lds(sqp_group_kernel<Model, BOUNDED, XB, EXACT>, lds);
     if (rc) return rc;
-    sqp_group_kernel<Model, BOUNDED, XB><<<grid, block, lds, stream>>>(p, gwk);
+    sqp_group_kernel<Model, BOUNDED, XB, EXACT><<<grid, block, lds, stream>>>(p, gwk);
     return MMPC_OK;
 }
 
@@ -634,8 +677,13 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         if (rc) return rc;
         GroupWork gwk{lw.ws};
         dim3 grid(grid1d(B, kGroupsPerWave)), block(64);
+        const int hess = resolve_hessian(h, solver, bounded);
+        if (hess < 0) return hess;
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
+            if constexpr (exact_capable<M>()) {
+                if (hess == MMPC_HESSIAN_EXACT) return launch_group<M, false, false, true>(grid, block, lds, stream, p, gwk);
+            }
             if (xb) return launch_group<M, false, true>(grid, block, lds, stream, p, gwk);
             return bounded ? launch_group<M, true>(grid, block, lds, stream, p, gwk)
                            : launch_group<M, false>(grid, block, lds, stream, p, gwk);
@@ -646,6 +694,10 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
     }
     if (p.x_bounded && solver == MMPC_KKT_CONDENSED)
         return fail(MMPC_ERR_UNSUPPORTED, "state bounds need a Riccati solver (MMPC_KKT_RICCATI[_GROUP])");
+    {
+        const int hess = resolve_hessian(h, solver, bounded);   // EXACT requested on an unsupported solver
+        if (hess < 0) return hess;
+    }
     if (solver == MMPC_KKT_CONDENSED) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 is a Riccati-solver option");
 #if MMPC_BUILTIN_MODELS
@@ -718,6 +770,7 @@ void mmpc_default_opts(mmpc_opts* o) {
     o->kkt_solver = MMPC_KKT_AUTO;
     o->factor_fp32 = 0;
     o->init_states = MMPC_INIT_AS_GIVEN;
+    o->hessian = MMPC_HESSIAN_AUTO;
 }
 
 int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_handle** out) {
@@ -894,6 +947,14 @@ int mmpc_solve_batch_host(mmpc_handle* h, int64_t B, const double* x0, const dou
 int mmpc_resolve_kkt_solver(const mmpc_handle* h, int64_t B, int32_t* solver) {
     if (!h || !solver || B < 0) return fail(MMPC_ERR_INVALID_ARG, "bad argument");
     *solver = resolve_kkt_solver(h, B);
+    return MMPC_OK;
+}
+
+int mmpc_resolve_hessian(const mmpc_handle* h, int64_t B, int32_t u_bounded, int32_t* hessian) {
+    if (!h || !hessian || B < 0) return fail(MMPC_ERR_INVALID_ARG, "null argument or B < 0");
+    const int r = resolve_hessian(h, resolve_kkt_solver(h, B), u_bounded != 0);
+    if (r < 0) return r;
+    *hessian = r;
     return MMPC_OK;
 }
 

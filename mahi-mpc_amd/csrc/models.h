@@ -5,8 +5,11 @@
 // to C (ModelGenerator.cpp:235-259).  Here each model is a device template over
 // the scalar type (double or Dual<NX+NU>), compiled into the solver kernel.
 #pragma once
+#include <type_traits>
+
 #include "dual.h"
 #include "exo_model_gen.h"
+#include "two_link_hess_gen.h"
 
 namespace mmpc {
 
@@ -45,6 +48,22 @@ struct TwoLinkArm {
     // acceleration and its partials d acc/dq [NQ*NQ], d acc/dqd [NQ*NQ], d acc/du [NQ*NU] (row-major)
     MMPC_HD static void eval_acc_jac(const double* x, const double* u, double* acc, double* Fq, double* Fqd,
                                      double* Fu);
+    // W = sum_s lam[s] d^2 acc_s / d(x, u)^2 (6 x 6 row-major): the dynamics part of the Lagrangian Hessian
+    // (CasADi nlp_hess_l, ModelGenerator.cpp:238), symbolic code generated from the SX statement of :36-37
+    static constexpr bool kHasHess = true;
+    MMPC_HD static void eval_hess(const double* x, const double* u, const double* lam, double* W) {
+        TwoLinkArmHess::eval_hess(x, u, lam, W);
+    }
+};
+
+// Second derivatives available (Model::eval_hess): exact-Hessian SQP and mmpc_nlp_hess_batch
+template <class M, class = void>
+struct HasHess {
+    static constexpr bool value = false;
+};
+template <class M>
+struct HasHess<M, std::enable_if_t<M::kHasHess>> {
+    static constexpr bool value = true;
 };
 
 // Forward-mode Jacobian of a model written as a scalar template: values and the continuous-time

@@ -35,8 +35,13 @@ __host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int nq, int 
     return N * (3 * nx + (nx - nq) * (nq + (nx - nq) + nu) + 2 * nu) + 3 * (N + 1) * nx + (bounded ? N * nu : 0) +
            (linear ? (nx - nq) * (nq + (nx - nq) + nu) + nx : 0) + (xb ? 5 * N * (nx + nu) : 0);
 }
-// HBM workspace doubles per instance: K_k | kff_k per stage
-__host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) { return N * nu * (nx + nu + 1); }
+// exact Hessian (EXACT): per stage the x rows of W_k = h sum_s lam_{k+1,NQ+s} d^2 acc_s/d(x,u)^2 (nx x (nx+nu))
+// and its u-u block (nu x nu), written stage-parallel and read by the lane-distributed Riccati sweep
+__host__ __device__ constexpr int group_hess_doubles(int nx, int nu) { return nx * (nx + nu) + nu * nu; }
+// HBM workspace doubles per instance: K_k | kff_k per stage, then the W_k blocks per stage
+__host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) {
+    return N * nu * (nx + nu + 1) + N * group_hess_doubles(nx, nu);
+}
 
 struct GroupWork {
     double* ws;
@@ -123,7 +128,9 @@ __device__ __forceinline__ void group_model(bool lin, const double* lFq, const d
 
 // XB: state bounds (oracle solve_one_ip), the primal-dual interior-point variant for state AND control bounds;
 // BOUNDED: control bounds only (projected GN-SQP).  At most one of them.
-template <class Model, bool BOUNDED = false, bool XB = false>
+// EXACT: exact Hessian of the Lagrangian (mmpc_opts.hessian; oracle ORACLE_HESS_EXACT) -- unbounded solves of
+// models with second derivatives on the lane-distributed path.
+template <class Model, bool BOUNDED = false, bool XB = false, bool EXACT = false>
 __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork gw) {
     static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
@@ -166,6 +173,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const sBb = sSg + N * NY;
     double* const sZg = sBb + N * NY;
     double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
+    constexpr int KZ = NX + NU, HW = group_hess_doubles(NX, NU);
+    double* const wH = wK + N * NU * (NS + 1);  // EXACT: [N][HW] = W_k x rows [NX][KZ] | W_k uu block [NU][NU]
     const double* const trg = p.traj + ii * (int64_t)N * NX;
 
     const double* w = p.weights + ii * p.w_stride;
@@ -185,6 +194,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     //      all lanes; rows are exchanged with row_bcast.  Bounded / state-bounded solves keep
     //      the one-lane sweep below. ----
     constexpr bool DIST = (NS < G) && !BOUNDED && !XB;
+    static_assert(!EXACT || (DIST && HasHess<Model>::value), "exact Hessian: lane-distributed path, model eval_hess");
     const int r = gl;
     const bool lx = r < NX, lu = r >= NX && r < NS, la = r >= NQ && r < NX;
     const int rx = lx ? r : 0;                        // x row of this lane (clamped for address arithmetic)
@@ -790,6 +800,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 const double eb = lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0;   // x_N - r_{N-1}
                 lamr = Qr * (sD[N * NX + rx] + eb);
                 lmax = fmax(lmax, fabs(lamr));
+                if (EXACT && lx) sD[N * NX + rx] = lamr;   // lam_k replaces d_k (read one stage earlier)
             }
             const double Rmr = lu ? w[NX + NU + ru] : 0.0;   // Rm of this lane's u row
             const double upr = p.u_prev[ii * NU + ru];
@@ -842,11 +853,22 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     }
                     lamr = lx ? t0 + t1 : 0.0;
                     lmax = fmax(lmax, fabs(lamr));
+                    if (EXACT && lx) sD[k * NX + rx] = lamr;
                 }
             }
         };
-        auto backward_dist = [&]() {
+        // useW (EXACT): the stage Hessians W_k of wH enter P~ (x-x block), H_ww (u-u) and H_wx (u-x)
+        auto backward_dist = [&](bool useW) {
             double Prow[NS], pvr;
+            const double lxm = lx ? 1.0 : 0.0;
+            double nwr[KZ], nwu[NU * NU];   // W_k row rx and uu block, loaded one stage ahead from the workspace
+            auto load_w = [&](int k) {
+#pragma unroll
+                for (int j = 0; j < KZ; ++j) nwr[j] = lxm * wH[k * HW + rx * KZ + j];
+#pragma unroll
+                for (int j = 0; j < NU * NU; ++j) nwu[j] = wH[k * HW + NX * KZ + j];
+            };
+            if (EXACT && useW) load_w(N - 1);
 #pragma unroll
             for (int j = 0; j < NS; ++j) Prow[j] = j < NX ? qoh[j] : 0.0;   // P~_N = blkdiag(Q, 0)
             pvr = Qr * (lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0);   // Q (x_N - r_{N-1})
@@ -872,6 +894,14 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 const double xk = sX[k * NX + rx], trm = tr[km * NX + rx];
                 const double exr = lx ? xk - trm : 0.0;
                 const double duu = sU[k * NU + ru] - sU[km * NU + ru];
+                double wr[KZ], wu[NU * NU];
+                if constexpr (EXACT) {
+#pragma unroll
+                    for (int j = 0; j < KZ; ++j) wr[j] = useW ? nwr[j] : 0.0;
+#pragma unroll
+                    for (int j = 0; j < NU * NU; ++j) wu[j] = useW ? nwu[j] : 0.0;
+                    if (useW) load_w(k > 0 ? k - 1 : 0);
+                }
                 // T = P~ [B; I] (row r), mv = P~_x. c + p~ (row r)
                 double T[NU], mv = pvr;
 #pragma unroll
@@ -899,6 +929,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                         for (int s2 = 0; s2 < NA; ++s2) t = fma(hFu[s2 * NU + a], Tb[NQ + s2][b], t);
                         if (a == b) t += R[a] + Rm[a];
+                        if constexpr (EXACT) t += wu[a * NU + b];
                         Hww[a][b] = t;
                         Hww[b][a] = t;
                     }
@@ -915,6 +946,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                     for (int q = 0; q < NX; ++q) tb[q] = Tb[q][a];
                     Ycol[a] = colA(T[a], acol, tb) - rdg[a];
+                    if constexpr (EXACT) Ycol[a] += wr[NX + a];   // H_wx[a][r] += W_ux[a][r] (x-lanes; 0 else)
                 }
                 // Kcol = H_ww^-1 Ycol (this lane's column of K~), kff = H_ww^-1 h_w (redundant)
                 double Kcol[NU], kff[NU], Ku[NU][NU];
@@ -1018,6 +1050,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                 for (int j = 0; j < NS; ++j) {
                     double v = j < NX ? Pn[j] + qoh[j] : rdg[j - NX];
+                    if constexpr (EXACT) {
+                        if (j < NX) v += wr[j];   // W_xx row r
+                    }
 #pragma unroll
                     for (int a = 0; a < NU; ++a) v = fma(-Ycol[a], j < NX ? Kb[a][j] : Ku[a][j - NX], v);
                     Prow[j] = v;
@@ -1106,7 +1141,41 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             break;
         }
         MMPC_PHASE(9);
-        if constexpr (DIST) backward_dist();   // Riccati sweep (fact_ok is uniform over the group)
+        if constexpr (EXACT) {
+            // stage-parallel: W_k = h sum_s lam_{k+1,NQ+s} d^2 acc_s/d(x_k,u_k)^2 (lam from the adjoint, in sD)
+            __builtin_amdgcn_wave_barrier();
+            for (int k = gl; k < N; k += G) {
+                double x[NX], u[NU], la[NA], W[KZ * KZ];
+#pragma unroll
+                for (int r2 = 0; r2 < NX; ++r2) x[r2] = sX[k * NX + r2];
+#pragma unroll
+                for (int c = 0; c < NU; ++c) u[c] = sU[k * NU + c];
+#pragma unroll
+                for (int s2 = 0; s2 < NA; ++s2) la[s2] = h * sD[(k + 1) * NX + NQ + s2];
+                Model::eval_hess(x, u, la, W);
+                double* const dst = wH + k * HW;
+#pragma unroll
+                for (int r2 = 0; r2 < NX; ++r2)
+#pragma unroll
+                    for (int j = 0; j < KZ; ++j) dst[r2 * KZ + j] = W[r2 * KZ + j];
+#pragma unroll
+                for (int a = 0; a < NU; ++a)
+#pragma unroll
+                    for (int b = 0; b < NU; ++b) dst[NX * KZ + a * NU + b] = W[(NX + a) * KZ + NX + b];
+            }
+            // the stores of the other lanes of this wave must be visible to the sweep's loads
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        }
+        if constexpr (DIST) {   // Riccati sweep (fact_ok is uniform over the group)
+            backward_dist(EXACT);
+            // exact KKT matrix not positive definite on the null space: this iteration takes the Gauss-Newton step
+            // (oracle solve_one: Cholesky of the exact condensed Hessian fails -> Gauss-Newton)
+            if (EXACT && !fact_ok) {
+                fact_ok = 1;
+                backward_dist(false);
+            }
+        }
         if (!fact_ok) {
             status = ST_FACT_FAILED;
             break;
@@ -1123,6 +1192,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             // K from the workspace), x-lanes dx_{k+1} = A dx + B du + c.  A dx_k + B du_k goes to sD[k+1] (d is
             // dead after the backward sweep) for the directional derivative below.
             if (fact_ok) {
+                // K_k columns were stored by the other lanes of this wave in the backward sweep
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 double sr = 0.0;
                 if (lx) sDX[rx] = 0.0;
                 constexpr int NK = NS + 1;

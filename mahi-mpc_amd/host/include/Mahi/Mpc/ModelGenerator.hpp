@@ -24,6 +24,13 @@
 namespace mahi {
 namespace mpc {
 
+// Device code of the weighted second derivatives of the accelerations (the part of CasADi's nlp_hess_l,
+// ModelGenerator.cpp:238, that depends on the dynamics): a member function
+//   MMPC_HD static void eval_hess(const double* x, const double* u, const double* lam, double* W)
+// with W = sum_{s < nx - nq} lam[s] d^2 x_dot[nq + s] / d(x, u)^2, (nx+nu) x (nx+nu) row-major (symmetric; the
+// kinematic rows q_dot = z[0:nq] are linear).  Symbolic: jacobian of jacobian of lam^T acc, CSE'd straight-line code.
+std::string emit_device_hessian(const SX& x, const SX& x_dot, const SX& u, int nq, const std::string& indent = "    ");
+
 class ModelGenerator {
 public:
     ModelGenerator(ModelParameters model_parameters, SX x, SX x_dot, SX u);  // ModelGenerator.hpp:23

@@ -41,6 +41,7 @@ class MmpcError(RuntimeError):
 
 KKT_AUTO, KKT_CONDENSED, KKT_RICCATI, KKT_RICCATI_GROUP = 0, 1, 2, 3
 INIT_AS_GIVEN, INIT_HOLD_X0 = 0, 1
+HESSIAN_AUTO, HESSIAN_GAUSS_NEWTON, HESSIAN_EXACT = 0, 1, 2
 MODEL_TWO_LINK_ARM, MODEL_EXO_ARM, MODEL_USER = 0, 1, 2
 USER_LIB_DIR = os.path.join(ROOT, "lib", "user")
 BUILTIN_MODELS = ("two_link_arm", "double_pendulum", "exo_arm", "exo")  # "mmpc_model" names libmmpc.so serves   # models generated from SX by ModelGenerator (make -C host user)
@@ -49,7 +50,7 @@ BUILTIN_MODELS = ("two_link_arm", "double_pendulum", "exo_arm", "exo")  # "mmpc_
 class Opts(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("device", C.c_int32), ("tol_grad", C.c_double),
                 ("tol_defect", C.c_double), ("kkt_solver", C.c_int32), ("factor_fp32", C.c_int32),
-                ("init_states", C.c_int32)]
+                ("init_states", C.c_int32), ("hessian", C.c_int32)]
 
 
 class ModelInfo(C.Structure):
@@ -109,6 +110,7 @@ def lib(path: str | None = None):
         L.mmpc_synth_batch.argtypes = [_vp, C.c_uint64, C.c_int64, C.c_int64] + [_vp] * 4
         L.mmpc_nlp_derivs_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 4
         L.mmpc_resolve_kkt_solver.argtypes = [_vp, C.c_int64, C.POINTER(C.c_int32)]
+        L.mmpc_resolve_hessian.argtypes = [_vp, C.c_int64, C.c_int32, C.POINTER(C.c_int32)]
         L.mmpc_set_state_bounds.argtypes = [_vp, _vp, _vp]
         L.mmpc_get_state_bounds.argtypes = [_vp, _vp, _vp]
         L.mmpc_status_string.argtypes = [C.c_int32]
@@ -195,7 +197,7 @@ class Solver:
     """One loaded model (the reference's ModelControl without the thread/bookkeeping)."""
 
     def __init__(self, model_json=None, json_text=None, max_iter=None, tol_grad=None, tol_defect=None,
-                 device=None, kkt_solver=None, factor_fp32=None, library=None, init_states=None):
+                 device=None, kkt_solver=None, factor_fp32=None, library=None, init_states=None, hessian=None):
         self._L = L = lib(library or (model_library(model_json) if model_json is not None else None))
         o = Opts()
         L.mmpc_default_opts(C.byref(o))
@@ -205,6 +207,8 @@ class Solver:
             o.factor_fp32 = int(factor_fp32)
         if init_states is not None:
             o.init_states = int(init_states)
+        if hessian is not None:
+            o.hessian = int(hessian)
         if max_iter is not None:
             o.max_iter = max_iter
         if tol_grad is not None:
@@ -303,6 +307,12 @@ class Solver:
         """KKT_* solver a solve of B instances runs (the AUTO choice resolved)."""
         v = C.c_int32()
         self._check(self._L.mmpc_resolve_kkt_solver(self._h, B, C.byref(v)))
+        return v.value
+
+    def hessian_for(self, B: int, u_bounded: bool = False) -> int:
+        """HESSIAN_GAUSS_NEWTON or HESSIAN_EXACT: what a solve of B instances runs (the AUTO choice resolved)."""
+        v = C.c_int32()
+        self._check(self._L.mmpc_resolve_hessian(self._h, B, int(bool(u_bounded)), C.byref(v)))
         return v.value
 
     def linearize_host(self, x, u):

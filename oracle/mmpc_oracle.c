@@ -111,6 +111,96 @@ static void two_link_dual(const dual* x, const dual* u, dual* xd) {
     xd[3] = ddiv(nB, den);
 }
 
+/* ---------------- second-order forward mode (value, gradient, Hessian over the 6 inputs x | u) ----------------
+ * Used for the exact Hessian of the Lagrangian (CasADi's nlp_hess_l, ModelGenerator.cpp:238; IPOPT's default
+ * hessian_approximation = exact, ModelControl.cpp:54-59).  Hessian stored full (symmetric) for clarity. */
+typedef struct { double v; double d[DK]; double H[DK][DK]; } hdual;
+
+static hdual hc(double c) { hdual r; memset(&r, 0, sizeof r); r.v = c; return r; }
+static hdual hvar(double v, int i) { hdual r = hc(v); r.d[i] = 1.0; return r; }
+static hdual hadd(hdual a, hdual b) {
+    hdual r; r.v = a.v + b.v;
+    for (int i = 0; i < DK; ++i) { r.d[i] = a.d[i] + b.d[i]; for (int j = 0; j < DK; ++j) r.H[i][j] = a.H[i][j] + b.H[i][j]; }
+    return r;
+}
+static hdual hscale(double s, hdual a) {
+    hdual r; r.v = s * a.v;
+    for (int i = 0; i < DK; ++i) { r.d[i] = s * a.d[i]; for (int j = 0; j < DK; ++j) r.H[i][j] = s * a.H[i][j]; }
+    return r;
+}
+static hdual hsub(hdual a, hdual b) { return hadd(a, hscale(-1.0, b)); }
+static hdual hmul(hdual a, hdual b) {
+    hdual r; r.v = a.v * b.v;
+    for (int i = 0; i < DK; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i];
+    for (int i = 0; i < DK; ++i)
+        for (int j = 0; j < DK; ++j)
+            r.H[i][j] = a.H[i][j] * b.v + a.v * b.H[i][j] + a.d[i] * b.d[j] + a.d[j] * b.d[i];
+    return r;
+}
+/* 1/b: d = -b'/b^2, H = 2 b' b'^T / b^3 - b''/b^2 */
+static hdual hinv(hdual b) {
+    hdual r; const double i1 = 1.0 / b.v, i2 = i1 * i1, i3 = i2 * i1;
+    r.v = i1;
+    for (int i = 0; i < DK; ++i) r.d[i] = -b.d[i] * i2;
+    for (int i = 0; i < DK; ++i)
+        for (int j = 0; j < DK; ++j) r.H[i][j] = 2.0 * b.d[i] * b.d[j] * i3 - b.H[i][j] * i2;
+    return r;
+}
+static hdual hdiv(hdual a, hdual b) { return hmul(a, hinv(b)); }
+/* f(a) with f' = f1, f'' = f2: d = f1 a', H = f1 a'' + f2 a' a'^T */
+static hdual hchain(hdual a, double f0, double f1, double f2) {
+    hdual r; r.v = f0;
+    for (int i = 0; i < DK; ++i) r.d[i] = f1 * a.d[i];
+    for (int i = 0; i < DK; ++i)
+        for (int j = 0; j < DK; ++j) r.H[i][j] = f1 * a.H[i][j] + f2 * a.d[i] * a.d[j];
+    return r;
+}
+static hdual hsin(hdual a) { return hchain(a, sin(a.v), cos(a.v), -sin(a.v)); }
+static hdual hcos(hdual a) { return hchain(a, cos(a.v), -sin(a.v), -cos(a.v)); }
+
+/* the accelerations of two_link_dual (examples/ex_model_generate.cpp:36-37) in second-order forward mode */
+static void two_link_hdual(const hdual* x, const hdual* u, hdual* acc) {
+    const double L = 1.0, m = 1.0, g = 9.81;
+    hdual qA = x[0], qB = x[1], dA = x[2], dB = x[3], TA = u[0], TB = u[1];
+    hdual cB = hcos(qB), sB = hsin(qB), cA = hcos(qA), cAB = hcos(hadd(qA, qB));
+    const double LLm = L * L * m, Lgm = L * g * m;
+    hdual dA2 = hmul(dA, dA), dB2 = hmul(dB, dB), dAdB = hmul(dA, dB), cBsB = hmul(cB, sB);
+    hdual den = hscale(LLm, hsub(hmul(cB, cB), hc(2.0)));
+    hdual nA = hsub(TA, TB);
+    nA = hsub(nA, hmul(TB, cB));
+    nA = hadd(nA, hscale(LLm, hmul(dA2, sB)));
+    nA = hadd(nA, hscale(LLm, hmul(dB2, sB)));
+    nA = hsub(nA, hscale(2.0 * Lgm, cA));
+    nA = hadd(nA, hscale(LLm, hmul(dA2, cBsB)));
+    nA = hadd(nA, hscale(2.0 * LLm, hmul(dAdB, sB)));
+    nA = hadd(nA, hscale(Lgm, hmul(cAB, cB)));
+    hdual nB = hsub(TA, hscale(3.0, TB));
+    nB = hadd(nB, hmul(TA, cB));
+    nB = hsub(nB, hscale(2.0, hmul(TB, cB)));
+    nB = hadd(nB, hscale(2.0 * Lgm, cAB));
+    nB = hadd(nB, hscale(3.0 * LLm, hmul(dA2, sB)));
+    nB = hadd(nB, hscale(LLm, hmul(dB2, sB)));
+    nB = hsub(nB, hscale(2.0 * Lgm, cA));
+    nB = hadd(nB, hscale(2.0 * LLm, hmul(dA2, cBsB)));
+    nB = hadd(nB, hscale(LLm, hmul(dB2, cBsB)));
+    nB = hsub(nB, hscale(2.0 * Lgm, hmul(cA, cB)));
+    nB = hadd(nB, hscale(2.0 * LLm, hmul(dAdB, sB)));
+    nB = hadd(nB, hscale(Lgm, hmul(cAB, cB)));
+    nB = hadd(nB, hscale(2.0 * LLm, hmul(dAdB, cBsB)));
+    acc[0] = hscale(-1.0, hdiv(nA, den));
+    acc[1] = hdiv(nB, den);
+}
+
+void oracle_two_link_hess(const double* x, const double* u, const double* lam, double* W) {
+    hdual xv[4], uv[2], acc[2];
+    for (int i = 0; i < 4; ++i) xv[i] = hvar(x[i], i);
+    for (int i = 0; i < 2; ++i) uv[i] = hvar(u[i], 4 + i);
+    two_link_hdual(xv, uv, acc);
+    /* rows 0, 1 of f (qdot) are linear: only the accelerations contribute */
+    for (int i = 0; i < DK; ++i)
+        for (int j = 0; j < DK; ++j) W[i * DK + j] = lam[2] * acc[0].H[i][j] + lam[3] * acc[1].H[i][j];
+}
+
 void oracle_two_link_jac(const double* x, const double* u, double* A, double* B, double* xdot) {
     dual xv[4], uv[2], xd[4];
     for (int i = 0; i < 4; ++i) xv[i] = dvar(x[i], i);
@@ -193,6 +283,26 @@ static void model_jac(const double* x, const double* u, double* A, double* B, do
         g_user_jac(x, u, A ? A : Af, B ? B : Bf, xdot);
     } else oracle_two_link_jac(x, u, A, B, xdot);
 }
+
+/* W = sum_r lam_r d^2 f_r / d(x,u)^2 ((nx+nu)^2, row-major); 0 when the model has no second derivatives */
+static oracle_user_hess_fn g_user_hess = NULL;
+int oracle_set_user_model_hess(oracle_user_hess_fn hess) {
+    g_user_hess = hess;
+    return 0;
+}
+static int model_has_hess(void) {
+    if (t_model == ORACLE_MODEL_TWO_LINK_ARM) return 1;
+    if (t_model == ORACLE_MODEL_USER) return g_user_hess != NULL;
+    return 0;
+}
+static int model_hess(const double* x, const double* u, const double* lam, double* W) {
+    if (t_model == ORACLE_MODEL_TWO_LINK_ARM) { oracle_two_link_hess(x, u, lam, W); return 1; }
+    if (t_model == ORACLE_MODEL_USER && g_user_hess) { g_user_hess(x, u, lam, W); return 1; }
+    return 0;
+}
+/* mmpc_opts.hessian (process-wide): ORACLE_HESS_GAUSS_NEWTON or ORACLE_HESS_EXACT */
+static int g_hess_mode = ORACLE_HESS_GAUSS_NEWTON;
+void oracle_set_hessian(int mode) { g_hess_mode = mode; }
 
 void oracle_two_link_xdot(const double* x, const double* u, double* xdot) {
     oracle_two_link_jac(x, u, NULL, NULL, xdot);
@@ -521,6 +631,45 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
          * ORACLE_BOUND_PASSES solves; the projected line search absorbs what is left). */
         int fact_fail = 0;
         if (has_b) { memcpy(s->H0, s->H, sizeof(double) * M * M); memcpy(s->g0, s->g, sizeof(double) * M); }
+        /* exact Hessian (ORACLE_HESS_EXACT): the QP in (dx, du) gains the stage term 1/2 [dx_k; du_k]^T W_k [..]
+         * with W_k = h sum_r lam_{k+1,r} d^2 f_r/d(x_k,u_k)^2 (J/2 scale, lam of step 5); condensed with
+         * dx_k = Gamma_k du + d_k (S_k du = [Gamma_k du; du_k]):  H += S_k^T W_k S_k,  g += S_k^T W_k [d_k; 0].
+         * The stop test above used the true reduced gradient; W only changes the step. */
+        const int use_exact = g_hess_mode == ORACLE_HESS_EXACT && !has_b && !g_lin && model_has_hess();
+        if (use_exact) {
+            memcpy(s->H0, s->H, sizeof(double) * M * M);
+            memcpy(s->g0, s->g, sizeof(double) * M);
+            const int K = NX + NU;
+            double W[(ORACLE_MAX_NX + ORACLE_MAX_NU) * (ORACLE_MAX_NX + ORACLE_MAX_NU)];
+            double* T = s->G;  /* Gamma is read below only through S; W S goes to a scratch row block */
+            double* WS = (double*)malloc(sizeof(double) * (size_t)K * M);
+            for (int k = 0; k < N; ++k) {
+                model_hess(s->X + k * NX, s->U + k * NU, s->lam + (k + 1) * NX, W);
+                /* WS = W S_k: S_k's x rows are Gamma rows of x_k (none for k = 0), its u rows select du_k */
+                for (int i = 0; i < K; ++i)
+                    for (int a = 0; a < M; ++a) {
+                        double t = 0.0;
+                        if (k >= 1)
+                            for (int q = 0; q < NX; ++q) t += W[i * K + q] * T[(size_t)((k - 1) * NX + q) * M + a];
+                        if (a / NU == k) t += W[i * K + NX + a % NU];
+                        WS[(size_t)i * M + a] = h * t;
+                    }
+                for (int a = 0; a < M; ++a) {
+                    /* (S^T W S)[a][b] = sum_i S[i][a] WS[i][b] ; (S^T W [d; 0])[a] = sum_i S[i][a] (W [d;0])[i] */
+                    for (int i = 0; i < K; ++i) {
+                        double sia;
+                        if (i < NX) sia = (k >= 1) ? T[(size_t)((k - 1) * NX + i) * M + a] : 0.0;
+                        else sia = (a == k * NU + (i - NX)) ? 1.0 : 0.0;
+                        if (sia == 0.0) continue;
+                        for (int b = 0; b < M; ++b) s->H[a * M + b] += sia * WS[(size_t)i * M + b];
+                        double wd = 0.0;
+                        for (int q = 0; q < NX; ++q) wd += W[i * K + q] * s->d[k * NX + q];
+                        s->g[a] += sia * h * wd;
+                    }
+                }
+            }
+            free(WS);
+        }
         for (int pass = 0;; ++pass) {
             if (has_b) {
                 if (pass) memcpy(s->H, s->H0, sizeof(double) * M * M);
@@ -537,7 +686,13 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
                     if (s->tgt[a] == s->tgt[a]) { s->H[a * M + a] = 1.0; s->g[a] = s->U[a] - s->tgt[a]; }
             }
             for (int a = 0; a < M; ++a) s->du[a] = -s->g[a];
-            if (chol_solve(M, s->H, s->du) != 0) { fact_fail = 1; break; }
+            if (chol_solve(M, s->H, s->du) != 0) {
+                if (!use_exact) { fact_fail = 1; break; }
+                /* exact KKT matrix not positive definite: this iteration takes the Gauss-Newton step */
+                memcpy(s->H, s->H0, sizeof(double) * M * M);
+                for (int a = 0; a < M; ++a) s->du[a] = -s->g0[a];
+                if (chol_solve(M, s->H, s->du) != 0) { fact_fail = 1; break; }
+            }
             if (!has_b || pass + 1 >= ORACLE_BOUND_PASSES) break;
             int added = 0;
             for (int a = 0; a < M; ++a) {

@@ -32,6 +32,21 @@ enum { ORACLE_MODEL_TWO_LINK_ARM = 0, ORACLE_MODEL_EXO_ARM = 1, ORACLE_MODEL_USE
  * sympy restatement of the same model (tests/test_sx_models.py). */
 typedef void (*oracle_user_jac_fn)(const double* x, const double* u, double* A, double* B, double* xdot);
 int oracle_set_user_model(int nx, int nu, oracle_user_jac_fn jac);
+/* second derivatives of the same generated model: W = sum_r lam[r] d^2 f_r / d(x,u)^2, (nx+nu)^2 row-major
+ * (NULL: the model has none and every solve uses the Gauss-Newton Hessian) */
+typedef void (*oracle_user_hess_fn)(const double* x, const double* u, const double* lam, double* W);
+int oracle_set_user_model_hess(oracle_user_hess_fn hess);
+
+/* Hessian of the SQP subproblem (mmpc_opts.hessian, process-wide for the following solves):
+ * GAUSS_NEWTON = J_F^T Q J_F + R terms only; EXACT = the Lagrangian Hessian (CasADi nlp_hess_l,
+ * ModelGenerator.cpp:238; IPOPT's default, ModelControl.cpp:54-59): adds, per stage, h sum_r lam_{k+1,r}
+ * d^2 f_r/d(x_k,u_k)^2 with lam the adjoint of the QP at the current iterate.  EXACT applies to unbounded,
+ * nonlinear solves of models with second derivatives (2-link arm, generated models); an iteration whose
+ * exact KKT matrix is not positive definite on the null space falls back to Gauss-Newton. */
+enum { ORACLE_HESS_GAUSS_NEWTON = 0, ORACLE_HESS_EXACT = 1 };
+void oracle_set_hessian(int mode);
+/* W = sum_r lam[r] d^2 f_r/d(x,u)^2 of the 2-link arm (6x6 row-major, x then u; lam[4]) */
+void oracle_two_link_hess(const double* x, const double* u, const double* lam, double* W);
 
 /* per-instance status, same numbering as include/mmpc.h */
 enum {

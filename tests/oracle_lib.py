@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
 
 NX, NU = 4, 2                       # 2-link arm (model 0)
 TWO_LINK, EXO, USER = 0, 1, 2
+HESS_GAUSS_NEWTON, HESS_EXACT = 0, 1   # oracle_set_hessian (mmpc_opts.hessian after resolution)
 DIMS = {TWO_LINK: (4, 2), EXO: (8, 4)}
 USER_DIR = os.path.join(ORACLE_DIR, "_user")
 _lib = None
@@ -56,6 +57,8 @@ def lib():
         L.oracle_synth_exo.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int, C.c_double, _dp, _dp, _dp]
         L.oracle_exo_jac.argtypes = [_dp, _dp, _dp, _dp, _dp]
         L.oracle_exo_mass.argtypes = [_dp, _dp]
+        L.oracle_two_link_hess.argtypes = [_dp, _dp, _dp, _dp]
+        L.oracle_set_hessian.argtypes = [C.c_int]
         _lib = L
     return _lib
 
@@ -72,7 +75,8 @@ class UserModelHost:
         L.user_model_dims(C.byref(dims, 0), C.byref(dims, 4), C.byref(dims, 8))
         self.nx, self.nu, self.nq = dims[0], dims[1], dims[2]
         self.na = self.nx - self.nq
-        for f, n in (("user_model_eval", 3), ("user_model_eval_acc_jac", 6), ("user_model_jac", 5)):
+        for f, n in (("user_model_eval", 3), ("user_model_eval_acc_jac", 6), ("user_model_jac", 5),
+                     ("user_model_hess", 4)):
             getattr(L, f).restype = None
             getattr(L, f).argtypes = [C.c_void_p] * n
         self.L, self.name = L, name
@@ -87,6 +91,13 @@ class UserModelHost:
         x, u = c64(x), c64(u)
         self.L.user_model_jac(x.ctypes.data, u.ctypes.data, A.ctypes.data, B.ctypes.data, xd.ctypes.data)
         return A.reshape(self.nx, self.nx), B.reshape(self.nx, self.nu), xd
+
+    def hess(self, x, u, lam):
+        """sum_r lam[r] d^2 f_r / d(x,u)^2 ((nx+nu)^2), lam over all nx rows"""
+        K = self.nx + self.nu
+        W = np.zeros(K * K)
+        self.L.user_model_hess(c64(x).ctypes.data, c64(u).ctypes.data, c64(lam).ctypes.data, W.ctypes.data)
+        return W.reshape(K, K)
 
     def acc_jac(self, x, u):
         na, nq, nu = self.na, self.nq, self.nu
@@ -103,6 +114,8 @@ def use_user_model(name) -> int:
     fn = C.cast(m.L.user_model_jac, C.c_void_p).value
     lib().oracle_set_user_model.argtypes = [C.c_int, C.c_int, C.c_void_p]
     assert lib().oracle_set_user_model(m.nx, m.nu, fn) == 0
+    lib().oracle_set_user_model_hess.argtypes = [C.c_void_p]
+    assert lib().oracle_set_user_model_hess(C.cast(m.L.user_model_hess, C.c_void_p).value) == 0
     _user["active"] = m  # keep the library loaded
     DIMS[USER] = (m.nx, m.nu)
     return USER
@@ -110,6 +123,13 @@ def use_user_model(name) -> int:
 
 def c64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def two_link_hess(x, u, lam):
+    """sum_r lam_r d^2 f_r / d(x,u)^2 of the 2-link arm (6x6)"""
+    W = np.zeros(36)
+    lib().oracle_two_link_hess(c64(x), c64(u), c64(lam), W)
+    return W.reshape(6, 6)
 
 
 def two_link_jac(x, u):
@@ -162,13 +182,21 @@ def synth(seed, first, B, N, h, model=TWO_LINK):
 
 def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=50,
                 tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK, x_lb=None, x_ub=None,
-                init_states=0):
+                init_states=0, hessian=HESS_GAUSS_NEWTON, solver=None):
+    """solver: the GPU mmpc.Solver being checked -- the oracle then runs the Hessian that solver resolves for this
+    batch (mmpc_resolve_hessian: exact for unbounded 2-link / generated-model solves on the group kernel)."""
+    if solver is not None:
+        fin = lambda b: b is not None and bool((np.abs(np.asarray(b, dtype=np.float64)) < 1e19).any())  # noqa: E731
+        hessian = {1: HESS_GAUSS_NEWTON, 2: HESS_EXACT}[solver.hessian_for(int(np.asarray(x0).reshape(-1, DIMS[model][0]).shape[0]),
+                                                                          fin(u_lb) or fin(u_ub))]
     lib().oracle_set_init_states(int(init_states))
+    lib().oracle_set_hessian(int(hessian))
     try:
         return _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_grad, tol_defect, nthreads,
                             is_linear, model, x_lb, x_ub)
     finally:
         lib().oracle_set_init_states(0)
+        lib().oracle_set_hessian(HESS_GAUSS_NEWTON)
 
 
 def _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_grad, tol_defect, nthreads,

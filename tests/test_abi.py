@@ -30,11 +30,12 @@ def test_library_is_gfx950_code_object(mmpc_mod):
 
 
 def test_abi_version_and_defaults(mmpc_mod):
-    assert mmpc_mod.lib().mmpc_abi_version() == 3
+    assert mmpc_mod.lib().mmpc_abi_version() == 4
     o = mmpc_mod.default_opts()
     assert o.max_iter == 50 and o.device == -1
     assert o.tol_grad == 1e-8 and o.tol_defect == 1e-10
     assert o.kkt_solver == mmpc_mod.KKT_AUTO
+    assert o.hessian == mmpc_mod.HESSIAN_AUTO
 
 
 def test_load_model_json_like_reference(model_json, mmpc_mod):
@@ -111,9 +112,12 @@ def test_workspace_size_and_solver_choice(tmp_path, model_json, mmpc_mod):
 def test_auto_solver_policy(tmp_path, model_json, mmpc_mod):
     """MMPC_KKT_AUTO (include/mmpc.h), resolved without a GPU"""
     m = mmpc_mod
-    s = m.Solver(model_json(N=30))                              # cfg#2 shape
-    assert s.kkt_solver_for(4096) == m.KKT_RICCATI_GROUP and s.kkt_solver_for(2560) == m.KKT_CONDENSED
-    assert s.kkt_solver_for(1) == m.KKT_CONDENSED and s.kkt_solver_for(65536) == m.KKT_RICCATI
+    s = m.Solver(model_json(N=30))                              # cfg#2 shape (exact Hessian: the group kernel)
+    assert s.kkt_solver_for(4096) == m.KKT_RICCATI_GROUP and s.kkt_solver_for(2560) == m.KKT_RICCATI_GROUP
+    assert s.kkt_solver_for(1) == m.KKT_RICCATI_GROUP and s.kkt_solver_for(65536) == m.KKT_RICCATI
+    s = m.Solver(model_json(N=30, name="gn"), hessian=m.HESSIAN_GAUSS_NEWTON)   # Gauss-Newton: condensed small B
+    assert s.kkt_solver_for(2560) == m.KKT_CONDENSED and s.kkt_solver_for(1) == m.KKT_CONDENSED
+    assert s.kkt_solver_for(4096) == m.KKT_RICCATI_GROUP
     s = m.Solver(model_json(N=60))                              # N*nu > 64
     assert s.kkt_solver_for(64) == m.KKT_RICCATI_GROUP and s.kkt_solver_for(16384) == m.KKT_RICCATI_GROUP
     assert s.kkt_solver_for(16667) == m.KKT_RICCATI
@@ -124,6 +128,30 @@ def test_auto_solver_policy(tmp_path, model_json, mmpc_mod):
     assert m.Solver(p).kkt_solver_for(4096) == m.KKT_RICCATI_GROUP and m.Solver(p).kkt_solver_for(8192) == m.KKT_RICCATI
     for k in (m.KKT_CONDENSED, m.KKT_RICCATI, m.KKT_RICCATI_GROUP):
         assert m.Solver(model_json(N=30), kkt_solver=k).kkt_solver_for(4096) == k
+
+
+def test_hessian_policy(tmp_path, model_json, mmpc_mod):
+    """mmpc_opts.hessian (include/mmpc.h) resolved without a GPU: AUTO = exact for unbounded nonlinear 2-link solves
+    on the group kernel, Gauss-Newton for bounded / linear / exo / lane-kernel solves; EXACT where unsupported is
+    an API error."""
+    m = mmpc_mod
+    s = m.Solver(model_json(N=30))
+    assert s.hessian_for(4096) == m.HESSIAN_EXACT and s.hessian_for(64) == m.HESSIAN_EXACT
+    assert s.hessian_for(4096, u_bounded=True) == m.HESSIAN_GAUSS_NEWTON
+    assert s.hessian_for(65536) == m.HESSIAN_GAUSS_NEWTON                 # lane kernel
+    assert m.Solver(model_json(N=30, name="lin", is_linear=True)).hessian_for(64) == m.HESSIAN_GAUSS_NEWTON
+    assert m.Solver(model_json(N=30, name="gn"), hessian=m.HESSIAN_GAUSS_NEWTON).hessian_for(4096) == 1
+    p = m.write_model_json(str(tmp_path / "exo20.json"), "exo20", 8, 4, 2000, 20, model="exo_arm")
+    assert m.Solver(p).hessian_for(4096) == m.HESSIAN_GAUSS_NEWTON
+    with pytest.raises(m.MmpcError) as ei:
+        m.Solver(p, hessian=m.HESSIAN_EXACT).hessian_for(4096)
+    assert ei.value.code == -4
+    with pytest.raises(m.MmpcError):
+        m.Solver(model_json(N=30, name="bad"), hessian=7)
+    s = m.Solver(model_json(N=30, name="ex"), hessian=m.HESSIAN_EXACT)
+    assert s.hessian_for(4096) == m.HESSIAN_EXACT
+    with pytest.raises(m.MmpcError):
+        s.hessian_for(4096, u_bounded=True)
 
 
 def test_invalid_opts_rejected(model_json, mmpc_mod):

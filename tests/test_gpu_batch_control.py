@@ -44,7 +44,7 @@ def targets(N, h, t, phase):
     return rows
 
 
-def oracle_loops(oracle, B, N, h, sim_s):
+def oracle_loops(oracle, B, N, h, sim_s, hessian=0):
     state = np.array([[0.05 * math.sin(1.3 * b + 0.7 * j) for j in range(4)] for b in range(B)])
     control = np.zeros((B, 2))
     V = None
@@ -56,7 +56,7 @@ def oracle_loops(oracle, B, N, h, sim_s):
         t = t_us * 1e-6
         if cycle % 5 == 0:
             tr = np.array([targets(N, h, t, 0.1 * b) for b in range(B)])
-            r = oracle.solve_batch(N, h, state, control, tr, np.array(WEIGHTS_CFG), V=V)
+            r = oracle.solve_batch(N, h, state, control, tr, np.array(WEIGHTS_CFG), V=V, hessian=hessian)
             V, res_t_us = r["V"], t_us
         times = [res_t_us + int(round(h * 1e6)) * i for i in range(N)]
         i = 0
@@ -95,7 +95,9 @@ def test_batch_sync_loops_match_oracle(which, oracle, tmp_path):
     B, N, h, sim = 64, 20, 0.002, 0.1
     model = MODEL if which == "generated" else builtin_model_dir(tmp_path)
     per_tick, status, final = parse_sync(run(model, B, sim, "sync"), B)
-    ref_tick, ref_final = oracle_loops(oracle, B, N, h, sim)
+    import mmpc
+    hess = mmpc.Solver(model + ".json").hessian_for(B)   # what the loop's B-instance solves run
+    ref_tick, ref_final = oracle_loops(oracle, B, N, h, sim, hessian=hess - 1)
     assert (status == 0).all()
     assert per_tick.shape == ref_tick.shape
     np.testing.assert_allclose(per_tick, ref_tick, rtol=1e-7, atol=1e-9)

@@ -38,9 +38,9 @@ def test_init_hold_matches_oracle(kkt, bounds, model_json, mmpc_mod, oracle):
     x0, up, tr = oracle.synth(20250213, 0, B, N, h)
     w = np.array(WEIGHTS_CFG)
     g = s.solve_batch_host(x0, up, tr, w, **kw)
-    o = oracle.solve_batch(N, h, x0, up, tr, w, init_states=1, max_iter=100, **okw)
+    o = oracle.solve_batch(N, h, x0, up, tr, w, init_states=1, max_iter=100, solver=s, **okw)
     compare(g, o)
-    ref = oracle.solve_batch(N, h, x0, up, tr, w, max_iter=100, **okw)  # the default initialisation
+    ref = oracle.solve_batch(N, h, x0, up, tr, w, max_iter=100, solver=s, **okw)  # the default initialisation
     assert np.abs(g["V"] - ref["V"]).max() / np.abs(ref["V"]).max() < 1e-7
 
 

@@ -120,7 +120,7 @@ def test_solve_vs_scipy_golden(which, golden_cfg1, golden_cfg2, model_json, mmpc
     assert _rel(r["V"], Vg).max() < 1e-6
     J, dinf = oracle.nlp_eval(g["N"], g["h"], r["V"][0], up[0], tr[0], np.array(g["weights"]))
     assert J == pytest.approx(Jg[0], rel=1e-8)
-    o = oracle.solve_batch(g["N"], g["h"], x0, up, tr, np.array(g["weights"]))
+    o = oracle.solve_batch(g["N"], g["h"], x0, up, tr, np.array(g["weights"]), solver=s)
     _compare(r, o, min_same=1.0)
 
 
@@ -142,7 +142,7 @@ def test_cfg2_full_batch_vs_oracle(model_json, mmpc_mod, oracle, torch_cuda):
     torch.cuda.synchronize()
     gpu = dict(V=V.cpu().numpy(), status=st.cpu().numpy(), iters=it.cpu().numpy(), kkt=kkt.cpu().numpy())
     xo, uo, to = x0.cpu().numpy(), up.cpu().numpy(), tr.cpu().numpy()
-    orc = oracle.solve_batch(N, H, xo, uo, to, np.array(WEIGHTS_CFG))
+    orc = oracle.solve_batch(N, H, xo, uo, to, np.array(WEIGHTS_CFG), solver=s)
     nc = np.where((gpu["status"] != 0) | (orc["status"] != 0))[0]
     if len(nc) and os.environ.get("MMPC_TEST_DUMP"):
         os.makedirs("gpurun_out", exist_ok=True)
@@ -188,7 +188,7 @@ def test_horizons(N, model_json, mmpc_mod, oracle):
     s = mmpc_mod.Solver(model_json(N=N))
     w = np.array(WEIGHTS_CFG)
     r = s.solve_batch_host(x0, up, tr, w)
-    o = oracle.solve_batch(N, H, x0, up, tr, w)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, solver=s)
     _compare(r, o)
 
 
@@ -218,7 +218,7 @@ def test_per_instance_weights(model_json, mmpc_mod, oracle):
     w = np.tile(WEIGHTS_CFG, (64, 1)) * rng.uniform(0.5, 2.0, (64, 8))
     s = mmpc_mod.Solver(model_json())
     r = s.solve_batch_host(x0, up, tr, w)
-    o = oracle.solve_batch(30, H, x0, up, tr, w)
+    o = oracle.solve_batch(30, H, x0, up, tr, w, solver=s)
     _compare(r, o)
 
 
@@ -245,6 +245,6 @@ def test_nonfinite_and_max_iter(model_json, mmpc_mod, oracle):
     assert list(r["status"]) == [0, 3, 3, 0]
     s2 = mmpc_mod.Solver(model_json(), max_iter=1)
     r2 = s2.solve_batch_host(x0[[0, 3]], up[[0, 3]], tr[[0, 3]], np.array(WEIGHTS_CFG))
-    o2 = oracle.solve_batch(30, H, x0[[0, 3]], up[[0, 3]], tr[[0, 3]], np.array(WEIGHTS_CFG), max_iter=1)
+    o2 = oracle.solve_batch(30, H, x0[[0, 3]], up[[0, 3]], tr[[0, 3]], np.array(WEIGHTS_CFG), max_iter=1, solver=s2)
     assert (r2["status"] == 1).all() and (r2["iters"] == 1).all()
     assert _rel(r2["V"], o2["V"]).max() < 1e-9

@@ -198,8 +198,9 @@ def test_riccati_two_link_long_horizons(N, model_json, mmpc_mod, oracle):
     # beyond the condensed kernel's N*nu <= 64: MMPC_KKT_AUTO selects the Riccati kernel
     x0, up, tr = oracle.synth(21, 0, 96, N, H)
     w = np.array(WEIGHTS_CFG)
-    r = mmpc_mod.Solver(model_json(N=N)).solve_batch_host(x0, up, tr, w)
-    o = oracle.solve_batch(N, H, x0, up, tr, w)
+    s = mmpc_mod.Solver(model_json(N=N))
+    r = s.solve_batch_host(x0, up, tr, w)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, solver=s)
     _compare(r, o)
 
 
@@ -276,8 +277,9 @@ def test_fp32_factor_is_riccati_only(model_json, mmpc_mod, oracle):
 def test_group_kernel_vs_oracle(N, B, model_json, mmpc_mod, oracle):
     x0, up, tr = oracle.synth(20250213, 3, B, N, H)
     w = np.array(WEIGHTS_CFG)
-    r = mmpc_mod.Solver(model_json(N=N), kkt_solver=mmpc_mod.KKT_RICCATI_GROUP).solve_batch_host(x0, up, tr, w)
-    o = oracle.solve_batch(N, H, x0, up, tr, w)
+    s = mmpc_mod.Solver(model_json(N=N), kkt_solver=mmpc_mod.KKT_RICCATI_GROUP)
+    r = s.solve_batch_host(x0, up, tr, w)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, solver=s)
     _compare(r, o)
 
 
@@ -294,7 +296,7 @@ def test_group_kernel_linear_weights_bounds_nonfinite_warmstart(model_json, mmpc
     wi = np.tile(WEIGHTS_CFG, (64, 1)) * rng.uniform(0.5, 2.0, (64, 8))
     s = mmpc_mod.Solver(model_json(N=30), kkt_solver=G)
     r = s.solve_batch_host(x0, up, tr, wi)
-    _compare(r, oracle.solve_batch(30, H, x0, up, tr, wi))
+    _compare(r, oracle.solve_batch(30, H, x0, up, tr, wi, solver=s))
     r2 = s.solve_batch_host(x0, up, tr, wi, V=r["V"])
     assert (r2["iters"] == 0).all() and (r2["status"] == 0).all()
     np.testing.assert_array_equal(r2["V"], r["V"])

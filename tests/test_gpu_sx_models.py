@@ -68,7 +68,7 @@ def test_generated_model_solve_matches_oracle(name, kkt, mmpc_mod, oracle):
     x0, up, tr = instances(s.nx, s.nu, B, s.N, s.h)
     w = weights(s.nx, s.nu)
     g = s.solve_batch_host(x0, up, tr, w)
-    o = oracle.solve_batch(s.N, s.h, x0, up, tr, w, model=mid)
+    o = oracle.solve_batch(s.N, s.h, x0, up, tr, w, model=mid, solver=s)
     compare(g, o)
     assert np.array_equal(g["V"][:, :s.nx], x0)  # x_0 pinned (ModelControl.cpp:144-145)
     s.close()

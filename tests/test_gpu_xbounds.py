@@ -135,12 +135,13 @@ def test_exo_state_bounds_lane(mmpc_mod, oracle, tmp_path):
 
 
 def test_state_bounds_api(model_json, mmpc_mod):
-    s = mmpc_mod.Solver(model_json(N=10))
+    s = mmpc_mod.Solver(model_json(N=10), hessian=mmpc_mod.HESSIAN_GAUSS_NEWTON)  # AUTO: condensed for small B
     lb, ub = s.state_bounds()
     assert np.isinf(lb).all() and np.isinf(ub).all()
     assert s.kkt_solver_for(64) == mmpc_mod.KKT_CONDENSED
     s.set_state_bounds([-1.0] * 4, [1.0] * 4)
     assert s.kkt_solver_for(64) == mmpc_mod.KKT_RICCATI_GROUP  # AUTO leaves the condensed solver
+    assert s.hessian_for(64) == mmpc_mod.HESSIAN_GAUSS_NEWTON
     with pytest.raises(mmpc_mod.MmpcError):
         s.set_state_bounds([1.0] * 4, [-1.0] * 4)
     forced = mmpc_mod.Solver(model_json(N=10, name="f", x_min=[-1.0] * 4, x_max=[1.0] * 4),
