@@ -222,6 +222,15 @@ int mmpc_nlp_derivs_batch(mmpc_handle* h, int64_t B, const double* V, const doub
                           const double* traj, const double* weights, int64_t weights_stride,
                           double* J, double* grad, double* jac_blocks, void* stream);
 
+/* nlp_hess_l of the reference's generated NLP (ModelGenerator.cpp:238; CasADi generate_dependencies): the Hessian of
+ * the Lagrangian lam_f J + lam_g^T g at V.  Output: the nonzero stage blocks on (x_k, u_k), [B][N][K][K] row-major
+ * (K = nx + nu, symmetric); the remaining nonzeros are constant, d^2 L / du_k du_{k-1} = -2 lam_f R, and x_N enters
+ * L linearly.  lam_g: DEVICE [B][N*nx] (g order, ModelGenerator.cpp:206) or NULL (zeros).  Needs second derivatives
+ * of the dynamics (built-in 2-link arm, SX-generated models; linear mode always): MMPC_ERR_UNSUPPORTED otherwise. */
+int mmpc_nlp_hess_batch(mmpc_handle* h, int64_t B, const double* V, const double* u_prev,
+                        const double* traj, const double* weights, int64_t weights_stride, double lam_f,
+                        const double* lam_g, double* hess_blocks, void* stream);
+
 /* Synthetic instances: cfg#2 recipe for the 2-link arm, cfg#3 recipe for the exo;
  * counter-based splitmix64(seed, first_index + b), so shards generate identical instances
  * whatever the GPU count.  DEVICE pointers. */

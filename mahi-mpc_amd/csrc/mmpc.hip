@@ -378,6 +378,72 @@ __global__ __launch_bounds__(256) void nlp_derivs_kernel(int64_t B, int N, doubl
     if (J) J[b] = Jv;
 }
 
+// nlp_hess_l of the generated NLP (ModelGenerator.cpp:238; CasADi's Hessian of the Lagrangian
+// lam_f J + lam_g^T g): the nonzero stage blocks, one thread per (instance, stage).  Block k on (x_k, u_k) [K x K]:
+//   lam_f [2 J_Fk^T Q J_Fk + blkdiag(0, 2R + 2Rm (+ 2R for k + 1 < N))] + h sum_r nu_r d^2 f_r/d(x_k,u_k)^2,
+//   nu = 2 lam_f Q e_k + lam_g,k,  J_Fk = [I + h f_x | h f_u],  e_k = F(x_k,u_k) - r_k;
+// the other nonzeros are constant (d^2/du_k du_{k-1} = -2 lam_f R) and x_N enters L linearly.
+template <class Model>
+__global__ __launch_bounds__(256) void nlp_hess_kernel(int64_t B, int N, double h, int is_linear,
+                                                       const double* __restrict__ V, const double* __restrict__ u_prev,
+                                                       const double* __restrict__ traj,
+                                                       const double* __restrict__ weights, int64_t w_stride,
+                                                       double lam_f, const double* __restrict__ lam_g, double* blocks) {
+    constexpr int NX = Model::NX, NU = Model::NU, ND = NX + NU, NQ = Model::NQ, NA = NX - NQ;
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= B * N) return;
+    const int64_t b = t / N;
+    const int k = static_cast<int>(t - b * N);
+    const int NV = NX * (N + 1) + NU * N;
+    const double* v = V + b * NV;
+    const double* w = weights + b * w_stride;
+    const double* up = u_prev + b * NU;
+    const double* xk = v + k * ND;
+    const double* uk = xk + NX;
+    double xd[NX], fx[NX * NX], fu[NX * NU];
+    if (!is_linear) {
+        model_eval_jac<Model>(xk, uk, xd, fx, fu);
+    } else {   // F_lin: A*, B*, xdot* at (x_0, u_prev)
+        double xs[NX], fxs[NX * NX], fus[NX * NU];
+        model_eval_jac<Model>(v, up, xs, fxs, fus);
+        for (int r = 0; r < NX; ++r) {
+            double s = xs[r];
+            for (int c = 0; c < NX; ++c) s += fxs[r * NX + c] * (xk[c] - v[c]);
+            for (int c = 0; c < NU; ++c) s += fus[r * NU + c] * (uk[c] - up[c]);
+            xd[r] = s;
+        }
+        for (int i = 0; i < NX * NX; ++i) fx[i] = fxs[i];
+        for (int i = 0; i < NX * NU; ++i) fu[i] = fus[i];
+    }
+    double JF[NX][ND], nu[NX];
+    for (int r = 0; r < NX; ++r) {
+        for (int c = 0; c < NX; ++c) JF[r][c] = (r == c ? 1.0 : 0.0) + h * fx[r * NX + c];
+        for (int c = 0; c < NU; ++c) JF[r][NX + c] = h * fu[r * NU + c];
+        const double e = xk[r] + h * xd[r] - traj[(b * N + k) * NX + r];
+        nu[r] = 2.0 * lam_f * w[r] * e + (lam_g ? lam_g[b * (int64_t)N * NX + k * NX + r] : 0.0);
+    }
+    double W[ND * ND];
+    for (int i = 0; i < ND * ND; ++i) W[i] = 0.0;
+    if constexpr (HasHess<Model>::value) {
+        if (!is_linear) {
+            double la[NA];
+            for (int s2 = 0; s2 < NA; ++s2) la[s2] = h * nu[NQ + s2];
+            Model::eval_hess(xk, uk, la, W);
+        }
+    }
+    double* out = blocks + t * (int64_t)(ND * ND);
+    for (int i = 0; i < ND; ++i)
+        for (int j = 0; j < ND; ++j) {
+            double s = W[i * ND + j];
+            for (int r = 0; r < NX; ++r) s += 2.0 * lam_f * w[r] * JF[r][i] * JF[r][j];
+            if (i == j && i >= NX) {
+                const int c = i - NX;
+                s += lam_f * (2.0 * w[NX + c] + 2.0 * w[NX + NU + c] + (k + 1 < N ? 2.0 * w[NX + c] : 0.0));
+            }
+            out[i * ND + j] = s;
+        }
+}
+
 __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -1053,6 +1119,36 @@ int mmpc_nlp_derivs_batch(mmpc_handle* h, int64_t B, const double* V, const doub
             B, h->info.num_shooting_nodes, h->info.step_size, h->info.is_linear, V, u_prev, traj, weights,
             weights_stride, J, grad, jac_blocks);
         return MMPC_OK;
+    });
+    if (rc) return rc;
+    MMPC_HIP(hipGetLastError());
+    return MMPC_OK;
+}
+
+int mmpc_nlp_hess_batch(mmpc_handle* h, int64_t B, const double* V, const double* u_prev, const double* traj,
+                        const double* weights, int64_t weights_stride, double lam_f, const double* lam_g,
+                        double* hess_blocks, void* stream) {
+    if (!h || B < 0) return fail(MMPC_ERR_INVALID_ARG, "null handle or B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!V || !u_prev || !traj || !weights || !hess_blocks) return fail(MMPC_ERR_INVALID_ARG, "null pointer");
+    const mmpc_model_info& mi = h->info;
+    if (weights_stride != 0 && weights_stride < mi.num_x + 2 * mi.num_u)
+        return fail(MMPC_ERR_INVALID_ARG, "weights_stride must be 0 or >= nx+2nu");
+    const int64_t n = B * mi.num_shooting_nodes;
+    if (n > 0x7fffffffLL * 256) return fail(MMPC_ERR_INVALID_ARG, "B*N too large");
+    int dev;
+    int rc = resolve_device(h, &dev);
+    if (rc) return rc;
+    DeviceGuard g(dev);
+    if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
+    rc = with_model(mi.model_id, [&](auto* m) {
+        using M = std::remove_pointer_t<decltype(m)>;
+        if (!HasHess<M>::value && !mi.is_linear)
+            return fail(MMPC_ERR_UNSUPPORTED, "nlp_hess: the model has no second derivatives");
+        nlp_hess_kernel<M><<<grid1d(n, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            B, mi.num_shooting_nodes, mi.step_size, mi.is_linear, V, u_prev, traj, weights, weights_stride, lam_f,
+            lam_g, hess_blocks);
+        return static_cast<int>(MMPC_OK);
     });
     if (rc) return rc;
     MMPC_HIP(hipGetLastError());

@@ -109,6 +109,7 @@ def lib(path: str | None = None):
         L.mmpc_nlp_eval_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 3
         L.mmpc_synth_batch.argtypes = [_vp, C.c_uint64, C.c_int64, C.c_int64] + [_vp] * 4
         L.mmpc_nlp_derivs_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 4
+        L.mmpc_nlp_hess_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64, C.c_double, _vp, _vp, _vp]
         L.mmpc_resolve_kkt_solver.argtypes = [_vp, C.c_int64, C.POINTER(C.c_int32)]
         L.mmpc_resolve_hessian.argtypes = [_vp, C.c_int64, C.c_int32, C.POINTER(C.c_int32)]
         L.mmpc_set_state_bounds.argtypes = [_vp, _vp, _vp]
@@ -269,6 +270,11 @@ class Solver:
         """J, dJ/dV and the defect-Jacobian stage blocks at V (device pointers; nlp_grad_f / nlp_jac_g)."""
         self._check(self._L.mmpc_nlp_derivs_batch(self._h, B, _ptr(V), _ptr(u_prev), _ptr(traj), _ptr(weights),
                                                   weights_stride, _ptr(J), _ptr(grad), _ptr(jac_blocks), stream))
+
+    def nlp_hess(self, B, V, u_prev, traj, weights, lam_f, lam_g, blocks, weights_stride=0, stream=None):
+        """nlp_hess_l stage blocks [B][N][K][K] of lam_f J + lam_g^T g at V (device pointers)."""
+        self._check(self._L.mmpc_nlp_hess_batch(self._h, B, _ptr(V), _ptr(u_prev), _ptr(traj), _ptr(weights),
+                                                weights_stride, float(lam_f), _ptr(lam_g), _ptr(blocks), stream))
 
     def linearize(self, B, x, u, A, Bm, xdot, stream=None):
         self._check(self._L.mmpc_linearize_batch(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xdot), stream))

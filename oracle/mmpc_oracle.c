@@ -410,6 +410,43 @@ void oracle_reduced_gradient(int model, int N, double h, const double* x0, const
     free(X); free(Ad); free(Bd);
 }
 
+/* nlp_hess_l (ModelGenerator.cpp:238): stage blocks on (x_k, u_k) of the Hessian of lam_f J + lam_g^T g at V,
+ * [N][K][K]; returns -1 when the model has no second derivatives (the Gauss-Newton part alone is not nlp_hess_l) */
+int oracle_nlp_hess(int model, int N, double h, const double* V, const double* u_prev, const double* traj,
+                    const double* w, double lam_f, const double* lam_g, double* blocks) {
+    (void)u_prev;  /* the Delta-u coupling -2 lam_f R is constant */
+    if (set_model(model) != 0 || !model_has_hess()) return -1;
+    const int K = NX + NU;
+    const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
+    for (int k = 0; k < N; ++k) {
+        const double* xk = V + k * ND;
+        const double* uk = xk + NX;
+        double A[ORACLE_MAX_NX * ORACLE_MAX_NX], Bc[ORACLE_MAX_NX * ORACLE_MAX_NU], xd[ORACLE_MAX_NX];
+        double nu[ORACLE_MAX_NX], W[(ORACLE_MAX_NX + ORACLE_MAX_NU) * (ORACLE_MAX_NX + ORACLE_MAX_NU)];
+        model_jac(xk, uk, A, Bc, xd);
+        for (int r = 0; r < NX; ++r) {
+            const double e = xk[r] + h * xd[r] - traj[k * NX + r];
+            nu[r] = h * (2.0 * lam_f * Q[r] * e + (lam_g ? lam_g[k * NX + r] : 0.0));
+        }
+        model_hess(xk, uk, nu, W);
+        double* out = blocks + (size_t)k * K * K;
+        for (int i = 0; i < K; ++i)
+            for (int j = 0; j < K; ++j) {
+                double t = W[i * K + j];
+                for (int r = 0; r < NX; ++r) {
+                    /* J_F = [I + h A | h B] */
+                    const double ji = i < NX ? (r == i ? 1.0 : 0.0) + h * A[r * NX + i] : h * Bc[r * NU + i - NX];
+                    const double jj = j < NX ? (r == j ? 1.0 : 0.0) + h * A[r * NX + j] : h * Bc[r * NU + j - NX];
+                    t += 2.0 * lam_f * Q[r] * ji * jj;
+                }
+                if (i == j && i >= NX)
+                    t += lam_f * (2.0 * R[i - NX] + 2.0 * Rm[i - NX] + (k + 1 < N ? 2.0 * R[i - NX] : 0.0));
+                out[i * K + j] = t;
+            }
+    }
+    return 0;
+}
+
 /* ---------------- dense GN-SQP for one instance ---------------- */
 typedef struct {
     int N, M;

@@ -85,6 +85,12 @@ void oracle_reduced_gradient(int model, int N, double h, const double* x0, const
                              const double* u_prev, const double* traj, const double* weights,
                              double* grad);
 
+/* nlp_hess_l (ModelGenerator.cpp:238): the (x_k, u_k) stage blocks [N][K][K] (K = nx+nu, row-major) of the Hessian
+ * of lam_f J + lam_g^T g at V (lam_g [N*nx], g order; may be NULL); d^2/du_k du_{k-1} = -2 lam_f R is constant.
+ * Returns -1 for a model without second derivatives. */
+int oracle_nlp_hess(int model, int N, double h, const double* V, const double* u_prev, const double* traj,
+                    const double* weights, double lam_f, const double* lam_g, double* blocks);
+
 /* Batched GN-SQP solve (the algorithm of DESIGN.md "Solver"), OpenMP over instances.
  * Layouts are instance-major:  x0[B][nx], u_prev[B][nu], traj[B][N*nx],
  * weights[w_stride==0 ? 1 : B][nx+2nu] = (Q | R | Rm), V[B][NV] (warm start in,

@@ -59,6 +59,8 @@ def lib():
         L.oracle_exo_mass.argtypes = [_dp, _dp]
         L.oracle_two_link_hess.argtypes = [_dp, _dp, _dp, _dp]
         L.oracle_set_hessian.argtypes = [C.c_int]
+        L.oracle_nlp_hess.argtypes = [C.c_int, C.c_int, C.c_double, _dp, _dp, _dp, _dp, C.c_double, C.c_void_p, _dp]
+        L.oracle_nlp_hess.restype = C.c_int
         _lib = L
     return _lib
 
@@ -162,6 +164,19 @@ def nlp_eval(N, h, V, u_prev, traj, weights, model=TWO_LINK):
     J = np.zeros(1); g = np.zeros(N * nx)
     lib().oracle_nlp_eval(model, N, h, c64(V), c64(u_prev), c64(traj).ravel(), c64(weights), J, g)
     return float(J[0]), g
+
+
+def nlp_hess(N, h, V, u_prev, traj, weights, lam_f=1.0, lam_g=None, model=TWO_LINK):
+    """nlp_hess_l stage blocks [N][K][K] of lam_f J + lam_g^T g at V"""
+    nx, nu = DIMS[model]
+    K = nx + nu
+    out = np.zeros(N * K * K)
+    lg = None if lam_g is None else c64(lam_g).reshape(-1)
+    rc = lib().oracle_nlp_hess(model, N, h, c64(V).reshape(-1), c64(u_prev), c64(traj).reshape(-1), c64(weights),
+                               float(lam_f), None if lg is None else lg.ctypes.data, out)
+    if rc != 0:
+        raise ValueError("model has no second derivatives")
+    return out.reshape(N, K, K)
 
 
 def reduced_gradient(N, h, x0, U, u_prev, traj, weights, model=TWO_LINK):
