@@ -388,7 +388,7 @@ def roofline(args, cfg, mmpc, ksolver, N, nx, nu, B, iters, kern_ms):
             for key, tj in json.load(open(args.traffic_json)).items():
                 if (key.startswith(f"{args.config}:{kname}") and isinstance(tj, dict) and tj.get("batch") == B
                         and tj.get("horizon") == N and tj.get("kernel_ms_at_measurement") is not None
-                        and abs(tj["kernel_ms_at_measurement"] - kern_ms) <= 0.25 * kern_ms):
+                        and abs(tj["kernel_ms_at_measurement"] - kern_ms) <= 0.05 * kern_ms):
                     traffic, traffic_src, pmc = tj.get("hbm_bytes_per_launch"), tj.get("source"), tj
         except (OSError, ValueError):
             traffic = None

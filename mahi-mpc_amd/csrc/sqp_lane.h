@@ -44,11 +44,13 @@ __host__ __device__ constexpr int lane_lin_doubles(int nx, int nu, int nq) {
 __host__ __device__ constexpr int lane_lin_stages(int nx, int nu, int nq, bool xb = false) {
     return (lane_lin_doubles(nx, nu, nq) + lane_stage_stride(nx, nu, xb) - 1) / lane_stage_stride(nx, nu, xb);
 }
-__host__ __device__ constexpr int lane_scratch_stages(int nx, int nu, bool xb = false) {
-    return (nx * nx + lane_stage_stride(nx, nu, xb) - 1) / lane_stage_stride(nx, nu, xb);
+__host__ __device__ constexpr bool lane_w_in_lds(int nx, int nu, int nq);
+__host__ __device__ constexpr int lane_scratch_stages(int nx, int nu, int nq, bool xb = false) {
+    return lane_w_in_lds(nx, nu, nq) ? 0 : (nx * nx + lane_stage_stride(nx, nu, xb) - 1) / lane_stage_stride(nx, nu, xb);
 }
 __host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int nq, int N, bool xb = false) {
-    return (N + 1 + lane_lin_stages(nx, nu, nq, xb) + lane_scratch_stages(nx, nu, xb)) * lane_stage_stride(nx, nu, xb);
+    return (N + 1 + lane_lin_stages(nx, nu, nq, xb) + lane_scratch_stages(nx, nu, nq, xb)) *
+           lane_stage_stride(nx, nu, xb);
 }
 template <int NX, int NU, bool XB = false>
 struct StageFields {
@@ -76,6 +78,22 @@ struct LaneWork {
 // packed upper-triangle index of (i, j), i <= j, of an n x n symmetric matrix
 __host__ __device__ constexpr int sym_idx(int n, int i, int j) {
     return i <= j ? i * n - i * (i - 1) / 2 + (j - i) : j * n - j * (j - 1) / 2 + (i - j);
+}
+
+// The P~_xu / P~_uu entries of the packed P~ are dead once G, H_ww, h_w and Y of a Riccati step are formed: their
+// slots hold the rows NQ..NX-1 of W = P_xx A (NA x NX) while P~_xx is rebuilt in place (sqp_lane_kernel, "W in
+// LDS").  i-th such slot in packed order; lane_w_in_lds: whether W's a-rows fit.
+__host__ __device__ constexpr int lane_dead_slot(int nx, int nu, int i) {
+    const int ns = nx + nu;
+    for (int a = 0; a < ns; ++a)
+        for (int b = (a > nx ? a : nx); b < ns; ++b) {
+            if (i == 0) return sym_idx(ns, a, b);
+            --i;
+        }
+    return -1;
+}
+__host__ __device__ constexpr bool lane_w_in_lds(int nx, int nu, int nq) {
+    return (nx - nq) * nx <= nx * nu + nu * (nu + 1) / 2;
 }
 
 // Products with the discrete stage matrices of a model with NQ kinematic rows (x = [q; z], qdot_i = z_i for
@@ -152,6 +170,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     const int lane = threadIdx.x;
     double* __restrict__ const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)lane_ws_doubles(NX, NU, NQ, N, XB) * 64);  // wave-uniform
     const int kScratch = N + 1 + lane_lin_stages(NX, NU, NQ, XB);  // first stage of the W = P_xx A scratch
+    constexpr bool WLDS = lane_w_in_lds(NX, NU, NQ);  // W's a-rows in the dead P~ slots, no HBM scratch
 #define ST(k, f, e) wsb[((int64_t)(k) * SS + (f) + (e)) * 64 + lane]  // one-off accesses
 #define SK(dk, f, e) sk[((dk) * SS + (f) + (e)) * 64]                   // stage k + dk inside a stage loop
 
@@ -352,6 +371,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         double mub_next = mub, amax = 1.0, az = 1.0, dbar = 0.0;  // interior point (XB)
         bool fact_ok = true, done = false;
         const double beps = BOUNDED ? fmin(kBoundEps, pg_prev) : 0.0;
+        constexpr bool FUSE_TRIAL = !BOUNDED && !XB;  // the alpha = 1 trial is evaluated inside the step sweep
+        double Jt1 = 0.0, ct1 = 0.0;
         // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
         double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
         #pragma unroll 1
@@ -562,6 +583,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     double pn[NS];
                     FT* const sw = reinterpret_cast<FT*>(stage_ptr(wsb, kScratch, SS, 0)) + lane;  // per-lane scratch stage
                     if (k >= 1) {
+                        if constexpr (!WLDS)
 #pragma unroll
                         for (int r = 0; r < NX; ++r) {
                             FT prow[NX], wrow[NX];
@@ -643,6 +665,59 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     }
                     if (k == 0) break;  // s_0 = 0: P~_0 is never used
                     // P~_k = blkdiag(A^T W + Q, R) - Y^T Y (old P is dead: overwrite it in place), p~_k = pn - Y^T yh
+                    if constexpr (WLDS) {
+                        // W in LDS: the a-rows of W (used by every output row) go to the dead P_xu / P_uu slots; the
+                        // q-rows are formed one at a time in registers, in descending order, each right before the
+                        // two output rows that use it (a and NQ + a): every P~_xx entry a later W row still reads
+                        // lies in a row not yet rewritten.
+                        auto WB = [&](int s2, int b) -> FT& { return Pl[lane_dead_slot(NX, NU, s2 * NX + b) * 64]; };
+#pragma unroll
+                        for (int s2 = 0; s2 < NA; ++s2) {
+                            FT prow[NX], wrow[NX];
+#pragma unroll
+                            for (int q = 0; q < NX; ++q) prow[q] = PS(NQ + s2, q);
+                            at_mul<NQ, NA, FT>(hf, fq, fqd, prow, wrow);
+#pragma unroll
+                            for (int b = 0; b < NX; ++b) WB(s2, b) = wrow[b];
+                        }
+                        auto out = [&](int a, int b, FT v) {
+                            v += (FT)((a == b) ? Q[a] + (XB ? SK(-1, SF::SG, a) : 0.0) : 0.0);
+#pragma unroll
+                            for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
+                            PS(a, b) = v;
+                        };
+                        // rows NQ + a for a >= NQ (first-order part beyond the kinematic pairs): W a-rows only
+#pragma unroll
+                        for (int a = NQ; a < NA; ++a)
+#pragma unroll
+                            for (int b = NQ + a; b < NX; ++b) {
+                                FT t = WB(a, b);
+#pragma unroll
+                                for (int s2 = 0; s2 < NA; ++s2) t = fma(fqd[s2 * NA + a], WB(s2, b), t);
+                                out(NQ + a, b, t);
+                            }
+#pragma unroll
+                        for (int a = NQ - 1; a >= 0; --a) {
+                            FT prow[NX], wt[NX];
+#pragma unroll
+                            for (int q = 0; q < NX; ++q) prow[q] = PS(a, q);
+                            at_mul<NQ, NA, FT>(hf, fq, fqd, prow, wt);   // row a of W
+#pragma unroll
+                            for (int b = a; b < NX; ++b) {   // output row a: W[a] + sum_s hFq[s][a] W[NQ+s]
+                                FT t = wt[b];
+#pragma unroll
+                                for (int s2 = 0; s2 < NA; ++s2) t = fma(fq[s2 * NQ + a], WB(s2, b), t);
+                                out(a, b, t);
+                            }
+#pragma unroll
+                            for (int b = NQ + a; b < NX; ++b) {   // output row NQ+a: h W[a] + W[NQ+a] + sum hFqd W
+                                FT t = fma(hf, wt[b], WB(a, b));
+#pragma unroll
+                                for (int s2 = 0; s2 < NA; ++s2) t = fma(fqd[s2 * NA + a], WB(s2, b), t);
+                                out(NQ + a, b, t);
+                            }
+                        }
+                    } else {
                     asm volatile("" ::: "memory");  // W comes back from memory, not from forwarded registers
 #pragma unroll
                     for (int b = 0; b < NX; ++b) {
@@ -657,6 +732,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                             for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
                             PS(a, b) = v;
                         }
+                    }
                     }
 #pragma unroll
                     for (int a = 0; a < NS; ++a) {
@@ -713,7 +789,11 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             }
 
             // ---- (3) forward: step (dx, du) and the directional derivative of J ----
+            // Unbounded solves also evaluate the line search's first trial (alpha = 1) here, stage by stage, with
+            // the operands already in registers: same values and summation order as the trial loop of (4).
             dJ = 0.0;
+            Jt1 = 0.0;
+            ct1 = 0.0;
             amax = 1.0;
             az = 1.0;
             dbar = 0.0;
@@ -731,15 +811,20 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 }
                 // software pipeline as in (1); the feedback gains K_k are consumed (and loaded) before the model
                 // evaluation, whose compute then covers the remaining loads of the stage
-                double xpf[NX], upf[NU];
+                double xpf[NX], upf[NU], umt[NU];
 #pragma unroll
                 for (int r = 0; r < NX; ++r) xpf[r] = ST(0, SF::X, r);
 #pragma unroll
-                for (int c = 0; c < NU; ++c) upf[c] = ST(0, SF::U, c);
+                for (int c = 0; c < NU; ++c) {
+                    upf[c] = ST(0, SF::U, c);
+                    umt[c] = up[c];
+                }
                 #pragma unroll 1
                 for (int k = 0; k < N; ++k) {
                     double* const sk = stage_ptr(wsb, k, SS, lane);
-                    double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU];
+                    double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU], dxk[NX];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) dxk[r] = dx[r];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         x[r] = xpf[r];
@@ -798,6 +883,30 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         um[c] = u[c];
                         dup[c] = du[c];
                     }
+                    if constexpr (FUSE_TRIAL) {   // trial point (x_k + dx_k, u_k + du_k), its defect to x_{k+1} + dx_{k+1}
+                        double xt[NX], ut[NU], xdt[NX];
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) xt[r] = x[r] + dxk[r];
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) ut[c] = u[c] + du[c];
+                        {
+                            double* nil_ = nullptr;
+                            STAGE_EVAL(xt, ut, xdt, nil_, nil_, nil_, false);
+                        }
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) {
+                            const double F = fma(h, xdt[r], xt[r]);
+                            const double er = F - rk[r];
+                            Jt1 = fma(er * Q[r], er, Jt1);
+                            ct1 += fabs(F - (xpf[r] + dx[r]));
+                        }
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) {
+                            const double dif = ut[c] - umt[c];
+                            Jt1 = fma(dif * R[c], dif, fma(ut[c] * Rm[c], ut[c], Jt1));
+                            umt[c] = ut[c];
+                        }
+                    }
                     if constexpr (XB) {  // fraction to the boundary of (x_{k+1} | u_k), barrier directional derivative
 #pragma unroll
                         for (int j = 0; j < NY; ++j)
@@ -821,6 +930,10 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         #pragma unroll 1
         for (int ls = 0; ls < 30; ++ls) {
             double Jt = 0.0, ct = 0.0, lt = 0.0, xk[NX], umt[NU], upf[NU], dupf[NU];
+            if (FUSE_TRIAL && ls == 0) {   // alpha = 1: evaluated in the step sweep
+                Jt = Jt1;
+                ct = ct1;
+            } else {
 #pragma unroll
             for (int r = 0; r < NX; ++r) xk[r] = ST(0, SF::X, r);  // dx_0 = 0
 #pragma unroll
@@ -867,6 +980,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
 #pragma unroll
                     for (int j = 0; j < NY; ++j) lt += ip_log_slacks(j < NX ? xn[j] : u[j - NX], yl[j], yu[j]);
                 }
+            }
             }
             const double phit = XB ? fma(mu, ct, fma(-2.0 * mub, lt, Jt)) : fma(mu, ct, Jt);
             const double noise = 1.0 + fabs(phi0);
