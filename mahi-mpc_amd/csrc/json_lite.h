@@ -45,6 +45,8 @@ public:
 private:
     const std::string& s_;
     size_t i_ = 0;
+    int depth_ = 0;  // nesting of the value being parsed (recursive descent: bounded so input cannot overflow the stack)
+    static constexpr int kMaxDepth = 64;
 
     [[noreturn]] void fail(const char* what) {
         throw std::runtime_error(std::string("json: ") + what + " at offset " + std::to_string(i_));
@@ -60,7 +62,14 @@ private:
         }
         return false;
     }
+    struct DepthGuard {
+        int& d;
+        explicit DepthGuard(int& d_) : d(d_) { ++d; }
+        ~DepthGuard() { --d; }
+    };
     Value value() {
+        DepthGuard guard(depth_);
+        if (depth_ > kMaxDepth) fail("nesting too deep");
         ws();
         if (i_ >= s_.size()) fail("unexpected end");
         char c = s_[i_];
