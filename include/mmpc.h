@@ -237,6 +237,29 @@ int mmpc_nlp_hess_batch(mmpc_handle* h, int64_t B, const double* V, const double
 int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t B, double* x0,
                      double* u_prev, double* traj, void* stream);
 
+/* ---- one process, several devices (the reference's per-instance worker loop of
+ *      ModelControl.cpp:75-112, batched and sharded) ----
+ * Contiguous split of B instances over n shards: shard i = [floor(i B / n), floor((i+1) B / n)) (first, count);
+ * the same partition as the multi-process path (mmpc/dist.py shard_strong).  Pure arithmetic, no device. */
+int mmpc_shard(int64_t B, int32_t n, int32_t i, int64_t* first, int64_t* count);
+
+typedef struct mmpc_multi mmpc_multi;
+/* One handle per listed device ordinal (each with its own stream, workspace and staging; a device may be listed
+ * more than once: its shards then run on concurrent streams).  opts.device is ignored. */
+int mmpc_multi_create(const char* model_json_path, const mmpc_opts* opts, const int32_t* devices, int32_t n_devices,
+                      mmpc_multi** out);
+int mmpc_multi_destroy(mmpc_multi* m);
+int mmpc_multi_num_devices(const mmpc_multi* m, int32_t* n);
+/* the handle of shard g (to reserve workspace, set state bounds or options device by device) */
+int mmpc_multi_handle(mmpc_multi* m, int32_t g, mmpc_handle** h);
+/* mmpc_solve_batch_host contract for the whole batch: shard g = mmpc_shard(B, n_devices, g) is solved on device g
+ * (H2D, solve, D2H on that device's stream, all devices concurrently) straight from/into the caller's arrays;
+ * synchronous.  Results equal a single-device solve of the same instances bit for bit. */
+int mmpc_multi_solve_batch_host(mmpc_multi* m, int64_t B, const double* x0, const double* u_prev,
+                                const double* traj, const double* weights, int64_t weights_stride,
+                                const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
+                                int32_t* iters, double* kkt_res);
+
 const char* mmpc_status_string(int32_t status);
 /* thread-local description of the last API error on this thread ("" if none) */
 const char* mmpc_last_error(void);

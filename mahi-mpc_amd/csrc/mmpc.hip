@@ -13,6 +13,7 @@
 #include <cstring>
 #include <fstream>
 #include <mutex>
+#include <thread>
 #include <sstream>
 #include <string>
 #include <type_traits>
@@ -1175,6 +1176,115 @@ int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t
         synth_two_link_kernel<<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
             seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
     MMPC_HIP(hipGetLastError());
+    return MMPC_OK;
+}
+
+// ---------------------------------------------------------------- multi-device (one process, G devices)
+int mmpc_shard(int64_t B, int32_t n, int32_t i, int64_t* first, int64_t* count) {
+    if (B < 0 || n < 1 || i < 0 || i >= n || !first || !count) return fail(MMPC_ERR_INVALID_ARG, "bad shard arguments");
+    if (B > (int64_t(1) << 40)) return fail(MMPC_ERR_INVALID_ARG, "B too large");
+    const int64_t lo = (static_cast<int64_t>(i) * B) / n, hi = (static_cast<int64_t>(i + 1) * B) / n;
+    *first = lo;
+    *count = hi - lo;
+    return MMPC_OK;
+}
+
+}  // extern "C"
+
+struct mmpc_multi {
+    std::vector<mmpc_handle*> h;  // one handle (own stream, workspace, staging) per listed device
+    std::vector<int32_t> dev;
+    std::mutex mu;                // one multi-device solve at a time
+};
+
+extern "C" {
+
+int mmpc_multi_create(const char* model_json_path, const mmpc_opts* opts, const int32_t* devices, int32_t n_devices,
+                      mmpc_multi** out) {
+    if (!model_json_path || !devices || n_devices < 1 || n_devices > 1024 || !out)
+        return fail(MMPC_ERR_INVALID_ARG, "bad multi-device arguments");
+    *out = nullptr;
+    std::unique_ptr<mmpc_multi> m(new mmpc_multi());
+    mmpc_opts o;
+    mmpc_default_opts(&o);
+    if (opts) o = *opts;
+    for (int32_t g = 0; g < n_devices; ++g) {
+        if (devices[g] < 0) {
+            for (mmpc_handle* x : m->h) mmpc_destroy(x);
+            return fail(MMPC_ERR_INVALID_ARG, "device ordinals must be >= 0");
+        }
+        o.device = devices[g];
+        mmpc_handle* h = nullptr;
+        const int rc = mmpc_create(model_json_path, &o, &h);
+        if (rc) {
+            for (mmpc_handle* x : m->h) mmpc_destroy(x);
+            return rc;
+        }
+        m->h.push_back(h);
+        m->dev.push_back(devices[g]);
+    }
+    *out = m.release();
+    return MMPC_OK;
+}
+
+int mmpc_multi_destroy(mmpc_multi* m) {
+    if (!m) return MMPC_OK;
+    for (mmpc_handle* h : m->h) mmpc_destroy(h);
+    delete m;
+    return MMPC_OK;
+}
+
+int mmpc_multi_num_devices(const mmpc_multi* m, int32_t* n) {
+    if (!m || !n) return fail(MMPC_ERR_INVALID_ARG, "null argument");
+    *n = static_cast<int32_t>(m->h.size());
+    return MMPC_OK;
+}
+
+int mmpc_multi_handle(mmpc_multi* m, int32_t g, mmpc_handle** h) {
+    if (!m || !h || g < 0 || g >= static_cast<int32_t>(m->h.size())) return fail(MMPC_ERR_INVALID_ARG, "bad device index");
+    *h = m->h[static_cast<size_t>(g)];
+    return MMPC_OK;
+}
+
+int mmpc_multi_solve_batch_host(mmpc_multi* m, int64_t B, const double* x0, const double* u_prev, const double* traj,
+                                const double* weights, int64_t weights_stride, const double* u_lb, const double* u_ub,
+                                double* V_inout, int32_t* status, int32_t* iters, double* kkt_res) {
+    if (!m) return fail(MMPC_ERR_INVALID_ARG, "null multi-device handle");
+    if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
+    if (B == 0) return MMPC_OK;
+    if (!x0 || !u_prev || !traj || !weights || !V_inout) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    std::lock_guard<std::mutex> lk(m->mu);
+    const mmpc_model_info& mi = m->h[0]->info;
+    const int64_t nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes, NV = mi.num_v;
+    const int32_t G = static_cast<int32_t>(m->h.size());
+    std::vector<int> rcs(static_cast<size_t>(G), MMPC_OK);
+    std::vector<std::string> errs(static_cast<size_t>(G));
+    // each device solves its contiguous shard of the host arrays on its own thread (H2D, solve, D2H on the
+    // handle's stream); shards are disjoint, so the results land in place without any assembly copy
+    auto work = [&](int32_t g) {
+        int64_t first = 0, count = 0;
+        mmpc_shard(B, G, g, &first, &count);
+        if (count == 0) return;
+        const int rc = mmpc_solve_batch_host(
+            m->h[static_cast<size_t>(g)], count, x0 + first * nx, u_prev + first * nu, traj + first * N * nx,
+            weights_stride ? weights + first * weights_stride : weights, weights_stride, u_lb, u_ub,
+            V_inout + first * NV, status ? status + first : nullptr, iters ? iters + first : nullptr,
+            kkt_res ? kkt_res + first : nullptr);
+        rcs[static_cast<size_t>(g)] = rc;
+        if (rc) errs[static_cast<size_t>(g)] = g_last_error;   // thread-local: carried back to the caller
+    };
+    if (G == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(static_cast<size_t>(G));
+        for (int32_t g = 0; g < G; ++g) th.emplace_back(work, g);
+        for (std::thread& t : th) t.join();
+    }
+    for (int32_t g = 0; g < G; ++g)
+        if (rcs[static_cast<size_t>(g)])
+            return fail(rcs[static_cast<size_t>(g)], "device " + std::to_string(m->dev[static_cast<size_t>(g)]) + ": " +
+                                                         errs[static_cast<size_t>(g)]);
     return MMPC_OK;
 }
 

@@ -110,6 +110,12 @@ def lib(path: str | None = None):
         L.mmpc_synth_batch.argtypes = [_vp, C.c_uint64, C.c_int64, C.c_int64] + [_vp] * 4
         L.mmpc_nlp_derivs_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 4
         L.mmpc_nlp_hess_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64, C.c_double, _vp, _vp, _vp]
+        L.mmpc_shard.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.mmpc_multi_create.argtypes = [C.c_char_p, C.POINTER(Opts), C.POINTER(C.c_int32), C.c_int32, C.POINTER(_vp)]
+        L.mmpc_multi_destroy.argtypes = [_vp]
+        L.mmpc_multi_num_devices.argtypes = [_vp, C.POINTER(C.c_int32)]
+        L.mmpc_multi_handle.argtypes = [_vp, C.c_int32, C.POINTER(_vp)]
+        L.mmpc_multi_solve_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 6
         L.mmpc_resolve_kkt_solver.argtypes = [_vp, C.c_int64, C.POINTER(C.c_int32)]
         L.mmpc_resolve_hessian.argtypes = [_vp, C.c_int64, C.c_int32, C.POINTER(C.c_int32)]
         L.mmpc_set_state_bounds.argtypes = [_vp, _vp, _vp]
@@ -330,6 +336,63 @@ class Solver:
         self._check(self._L.mmpc_linearize_batch_host(self._h, B, _ptr(x), _ptr(u), _ptr(A), _ptr(Bm), _ptr(xd)))
         # column-major per instance (CasADi DM order) -> (B, nx, nx) row-major views
         return (A.reshape(B, nx, nx).transpose(0, 2, 1), Bm.reshape(B, nu, nx).transpose(0, 2, 1), xd)
+
+
+def shard(B: int, n: int, i: int) -> tuple:
+    """(first, count) of shard i of B instances over n shards (mmpc_shard; the C-ABI's partition)."""
+    f, c = C.c_int64(), C.c_int64()
+    _check(lib().mmpc_shard(B, n, i, C.byref(f), C.byref(c)))
+    return f.value, c.value
+
+
+class MultiSolver:
+    """One process over several devices (mmpc_multi_*): contiguous shards, one handle and stream per device."""
+
+    def __init__(self, model_json, devices, **opts):
+        self._L = L = lib(model_library(model_json))
+        o = Opts()
+        L.mmpc_default_opts(C.byref(o))
+        for k, v in opts.items():
+            setattr(o, k, v)
+        devs = (C.c_int32 * len(devices))(*devices)
+        m = _vp()
+        _check(L.mmpc_multi_create(os.fsencode(model_json), C.byref(o), devs, len(devices), C.byref(m)), L)
+        self._m = m
+        info = ModelInfo()
+        h = _vp()
+        _check(L.mmpc_multi_handle(m, 0, C.byref(h)), L)
+        _check(L.mmpc_get_model_info(h, C.byref(info)), L)
+        self.nx, self.nu, self.N, self.NV = info.num_x, info.num_u, info.num_shooting_nodes, info.num_v
+
+    def num_devices(self) -> int:
+        n = C.c_int32()
+        _check(self._L.mmpc_multi_num_devices(self._m, C.byref(n)), self._L)
+        return n.value
+
+    def solve_batch_host(self, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None):
+        nx, nu, N, NV = self.nx, self.nu, self.N, self.NV
+        x0 = _f64(x0, (-1, nx))
+        B = x0.shape[0]
+        u_prev, traj, weights = _f64(u_prev, (B, nu)), _f64(traj, (B, N, nx)), _f64(weights)
+        ws = 0 if weights.ndim == 1 else weights.shape[-1]
+        V = np.zeros((B, NV)) if V is None else _f64(V, (B, NV)).copy()
+        st, it, kkt = np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(B)
+        lb = None if u_lb is None else _f64(u_lb)
+        ub = None if u_ub is None else _f64(u_ub)
+        _check(self._L.mmpc_multi_solve_batch_host(self._m, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights), ws,
+                                                   _ptr(lb), _ptr(ub), _ptr(V), _ptr(st), _ptr(it), _ptr(kkt)), self._L)
+        return dict(V=V, status=st, iters=it, kkt=kkt)
+
+    def close(self):
+        if getattr(self, "_m", None):
+            self._L.mmpc_multi_destroy(self._m)
+            self._m = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def flops_per_iteration(N: int, nx: int = 4, nu: int = 2) -> dict:

@@ -188,3 +188,21 @@ def test_flop_model(mmpc_mod):
     assert abs(mmpc_mod.survey_flops_per_iteration(50, 8, 4) - 9276266) <= 1
     r = mmpc_mod.riccati_flops_per_iteration(50, 8, 4)
     assert 0 < r["total"] < 9276266 / 30
+
+
+def test_shard_partition_matches_multiprocess_split(mmpc_mod):
+    """mmpc_shard (the multi-device C-ABI's partition) = mmpc/dist.py shard_strong for every (B, n, i), covers
+    [0, B) exactly once in order, ragged B included; invalid arguments are API errors (no device needed)."""
+    import mmpc.dist as mdist
+    for B in (0, 1, 5, 37, 4096, 65537):
+        for n in (1, 2, 3, 7, 8):
+            nxt = 0
+            for i in range(n):
+                f, c = mmpc_mod.shard(B, n, i)
+                assert (f, c) == mdist.shard_strong(B, i, n)
+                assert f == nxt and c >= 0
+                nxt = f + c
+            assert nxt == B
+    for bad in ((-1, 2, 0), (10, 0, 0), (10, 2, 2), (10, 2, -1)):
+        with pytest.raises(mmpc_mod.MmpcError):
+            mmpc_mod.shard(*bad)
