@@ -126,7 +126,7 @@ def launch(args, argv) -> int:
 
 
 # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1 only)
-def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect):
+def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1):
     """Oracle (oracle/liboracle.so: the same NLP and GN-SQP in plain C + OpenMP, dense condensed KKT) on a
     bounded sample of the same seeded workload, plus its agreement with the GPU on the shared instances."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -134,7 +134,9 @@ def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect):
     model = o.EXO if cfg["model"] == "exo_arm" else o.TWO_LINK
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     w = np.array(cfg["weights"])
-    kw = dict(nthreads=threads, model=model, tol_grad=tol_grad, tol_defect=tol_defect)
+    # the same SQP as the GPU: the Hessian the library resolved (mmpc_resolve_hessian: 1 Gauss-Newton, 2 exact)
+    kw = dict(nthreads=threads, model=model, tol_grad=tol_grad, tol_defect=tol_defect,
+              hessian=o.HESS_EXACT if hessian == 2 else o.HESS_GAUSS_NEWTON)
     n0 = 2 * threads
     x0, up, tr = o.synth(SEED, 0, n0, N, h, model=model)
     t = time.perf_counter()
@@ -155,6 +157,7 @@ def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect):
                 sample=f"first {n} {cfg['workload'].split(':')[0]} instances (seed {SEED}), cold start, {dt:.1f} s "
                        f"wall, {int((r['status'] == 0).sum())}/{n} converged; oracle GN-SQP with a DENSE condensed "
                        f"KKT (Cholesky of the N*nu Hessian, not the Riccati recursion the GPU runs), "
+                       f"{'exact' if hessian == 2 else 'Gauss-Newton'} Hessian as the GPU, "
                        f"{threads} OpenMP threads",
                 vs_gpu=dict(instances=int(m), max_rel_diff_V=float(rel.max()),
                             max_rel_diff_V_same_iters=float(rel[same_it].max()) if same_it.any() else None,
@@ -346,10 +349,12 @@ def run_rank(args):
     else:
         import mmpc
         out["kernel_ms"] = kern_ms
-        out["roofline"] = roofline(args, cfg, mmpc, ksolver, N, nx, nu, B, iters, kern_ms)
+        out["roofline"] = roofline(args, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms)
+    if args.config == "cfg5" and world == 1 and not standin:
+        out["tolerance_sweep"] = cfg5_sweep(path, cfg, B, x0, up, tr, w, args.hessian)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin:
         out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
-                                           tol_defect)
+                                           tol_defect, hess)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if not standin:
@@ -358,7 +363,47 @@ def run_rank(args):
         dist.destroy_process_group()
 
 
-def roofline(args, cfg, mmpc, ksolver, N, nx, nu, B, iters, kern_ms):
+def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3):
+    """SURVEY.md 8d cfg#5: the fp32-factor solve over the outer tolerance {1e-5, 1e-6, 1e-8} (tol_grad = tol,
+    tol_defect = tol / 100) -- % converged, mean / max SQP iterations, kernel ms (HIP events, median of `reps`) and
+    max_i ||V_i - V_i,fp64|| / ||V_i,fp64|| against the fp64-factor solve at the default tolerances."""
+    import torch
+    import mmpc
+
+    def run(tol, fp32):
+        s = mmpc.Solver(path, tol_grad=tol, tol_defect=tol / 100, factor_fp32=int(fp32))
+        s.reserve_workspace(B)
+        V = torch.zeros((B, s.NV), dtype=torch.float64, device=x0.device)
+        st = torch.zeros(B, dtype=torch.int32, device=x0.device)
+        it = torch.zeros(B, dtype=torch.int32, device=x0.device)
+        times = []
+        for _ in range(reps):
+            V.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            s.solve_batch(B, x0, up, tr, w, V, st, it, None)
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1))
+        s.close()
+        return V, st.cpu().numpy(), it.cpu().numpy(), float(np.median(times))
+
+    Vref, st_ref, it_ref, t_ref = run(1e-8, False)
+    nref = torch.linalg.vector_norm(Vref, dim=1)
+    rows = []
+    for tol in (1e-5, 1e-6, 1e-8):
+        V, st, it, t = run(tol, True)
+        rel = (torch.linalg.vector_norm(V - Vref, dim=1) / nref).max().item()
+        rows.append({"factor": "fp32", "tol_grad": tol, "tol_defect": tol / 100, "converged_pct": float((st == 0).mean() * 100),
+                     "mean_iters": float(it.mean()), "max_iters": int(it.max()), "kernel_ms": t,
+                     "max_rel_V_vs_fp64": rel})
+    rows.append({"factor": "fp64", "tol_grad": 1e-8, "tol_defect": 1e-10, "converged_pct": float((st_ref == 0).mean() * 100),
+                 "mean_iters": float(it_ref.mean()), "max_iters": int(it_ref.max()), "kernel_ms": t_ref,
+                 "max_rel_V_vs_fp64": 0.0})
+    return rows
+
+
+def roofline(args, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms):
     """FP64-VALU roofline of the solve kernel (the only kernel of a step besides a memset and the result pack).
 
     achieved = the kernel's OWN algorithmic flop count (mmpc.*_flops_per_iteration: structure-exploiting, no
@@ -369,7 +414,7 @@ def roofline(args, cfg, mmpc, ksolver, N, nx, nu, B, iters, kern_ms):
     algorithm-equivalent rate: it is NOT the work the kernel does."""
     riccati = ksolver in (2, 3)
     if riccati:
-        fl = mmpc.riccati_flops_per_iteration(N, nx, nu)
+        fl = mmpc.riccati_flops_per_iteration(N, nx, nu, exact=solver.hessian_for(B) == mmpc.HESSIAN_EXACT)
         model = "ExoArm" if cfg["model"] == "exo_arm" else "TwoLinkArm"
         if ksolver == 3:
             kname = f"sqp_group_kernel<{model}"

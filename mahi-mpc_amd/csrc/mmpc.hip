@@ -434,7 +434,7 @@ __global__ __launch_bounds__(256) void nlp_hess_kernel(int64_t B, int N, double 
     }
     double* out = blocks + t * (int64_t)(ND * ND);
     for (int i = 0; i < ND; ++i)
-        for (int j = 0; j < ND; ++j) {
+        for (int j = i; j < ND; ++j) {   // upper triangle, mirrored: the block is symmetric bit for bit
             double s = W[i * ND + j];
             for (int r = 0; r < NX; ++r) s += 2.0 * lam_f * w[r] * JF[r][i] * JF[r][j];
             if (i == j && i >= NX) {
@@ -442,6 +442,7 @@ __global__ __launch_bounds__(256) void nlp_hess_kernel(int64_t B, int N, double 
                 s += lam_f * (2.0 * w[NX + c] + 2.0 * w[NX + NU + c] + (k + 1 < N ? 2.0 * w[NX + c] : 0.0));
             }
             out[i * ND + j] = s;
+            out[j * ND + i] = s;
         }
 }
 

@@ -415,7 +415,7 @@ def flops_per_iteration(N: int, nx: int = 4, nu: int = 2) -> dict:
     return f
 
 
-def riccati_flops_per_iteration(N: int, nx: int = 8, nu: int = 4) -> dict:
+def riccati_flops_per_iteration(N: int, nx: int = 8, nu: int = 4, exact: bool = False) -> dict:
     """Algorithmic flop count (mul+add = 2) of ONE SQP iteration of the lane-per-instance Riccati kernel
     (sqp_lane.h), structure-exploiting for second-order models (A = [[I, hI],[hFq, I+hFqd]],
     B = [[0],[hFu]], nq = nx/2).  Model evaluations are excluded (SURVEY.md 8d counts them separately)."""
@@ -436,6 +436,8 @@ def riccati_flops_per_iteration(N: int, nx: int = 8, nu: int = 4) -> dict:
     st += nu * nu * (ns + 1)                  # back solve (K)
     st += ns * (ns + 1) // 2 * 2 * nu + ns * 2 * nu  # P~ = ... - Y^T Y, p~
     f["riccati"] = N * st
+    if exact:   # the stage Hessian W_k enters P~_xx, H_ww and H_wx (its evaluation is a model evaluation: excluded)
+        f["riccati"] += N * (nx * nx + nu * nu + nx * nu)
     f["step_recursion"] = N * (2 * nu * ns + at_mul + 2 * nq * nu + nx)
     f["merit"] = N * (4 * nx + 8 * nu)
     f["total"] = sum(f.values())

@@ -109,7 +109,7 @@ def test_nlp_hess(model, mmpc_mod, oracle, tmp_path):
     lam_f J + lam_g^T g against the oracle's (its own hyper-dual second derivatives for the 2-link arm; the host build
     of the generated header, itself pinned to sympy, for cart-pole) at 1e-12 relative; symmetric.  The exo model has
     no second derivatives: an API error, not a silent Gauss-Newton block."""
-    B, h, lam_f = 24, 0.002, 0.7
+    B, lam_f = 24, 0.7
     if model == "cart_pole":
         path = os.path.join(ROOT, "mahi-mpc_amd", "lib", "user", "cart_pole.json")
         if not os.path.exists(path):
@@ -139,6 +139,6 @@ def test_nlp_hess(model, mmpc_mod, oracle, tmp_path):
     torch.cuda.synchronize()
     H = out.cpu().numpy()
     for b in range(B):
-        ref = oracle.nlp_hess(N, h, V[b], up[b], tr[b], w, lam_f, lam[b], model=om)
+        ref = oracle.nlp_hess(N, s.h, V[b], up[b], tr[b], w, lam_f, lam[b], model=om)
         assert np.abs(H[b] - ref).max() <= 1e-12 * max(1.0, np.abs(ref).max()), b
         np.testing.assert_array_equal(H[b], H[b].transpose(0, 2, 1))
