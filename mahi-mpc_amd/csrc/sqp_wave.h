@@ -77,6 +77,16 @@ enum {
 constexpr double kBoundEps = 1e-6;
 constexpr int kBoundPasses = 4;
 __device__ __forceinline__ double proj(double v, double lb, double ub) { return v < lb ? lb : (v > ub ? ub : v); }
+
+// First SQP iteration: IPOPT's filter acceptance (Waechter & Biegler 2006, eqs. (18)-(21); oracle
+// first_iter_filter_accepts).  Its filter then holds only theta_max = 1e4 max(1, theta_0) and the cold start is far
+// from feasible (no switching to Armijo), so a trial (J_t, theta_t = |c_t|_1) is taken when theta_t <= theta_max and
+// theta_t <= (1 - 1e-5) theta_0 or J_t <= J_0 - 1e-5 theta_0.  Later iterations use the l1-merit Armijo test alone.
+__device__ __forceinline__ bool first_iter_filter_accepts(double J0, double c0, double Jt, double ct) {
+    if (!(isfinite(Jt) && isfinite(ct))) return false;
+    if (ct > 1e4 * fmax(1.0, c0)) return false;
+    return ct <= (1.0 - 1e-5) * c0 || Jt <= J0 - 1e-5 * c0;
+}
 // bound values of |b| >= 1e19 are infinite (IPOPT's convention); NaN marks a free control in hold fields
 template <int NU, bool BOUNDED>
 __device__ __forceinline__ void load_bounds(const SolveParams& p, double* lbv, double* ubv) {
@@ -886,7 +896,8 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
             // (it is a sum of ~200 terms), so such a step is taken whole, and the test allows 1e-13 |phi|
             // of roundoff.  Without this the test compares noise and alpha collapses.
             const double noise = 1.0 + fabs(phi0);
-            if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) {
+            if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise ||
+                (it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct))) {
                 accepted = true;
                 break;
             }

@@ -530,6 +530,15 @@ static int chol_solve(int M, double* H, double* b /* in: rhs, out: solution */) 
     return 0;
 }
 
+/* IPOPT's filter acceptance of a trial (J_t, theta_t = |c_t|_1) w.r.t. the first iterate (J_0, theta_0) -- the
+ * filter holds only (theta_max, -inf) then: theta_t <= theta_max = 1e4 max(1, theta_0), and theta_t <= (1 - 1e-5)
+ * theta_0 or J_t <= J_0 - 1e-5 theta_0 (gamma_theta = gamma_phi = 1e-5).  J-scale as the merit. */
+static int first_iter_filter_accepts(double J0, double c0, double Jt, double ct) {
+    if (!(isfinite(Jt) && isfinite(ct))) return 0;
+    if (ct > 1e4 * fmax(1.0, c0)) return 0;
+    return ct <= (1.0 - 1e-5) * c0 || Jt <= J0 - 1e-5 * c0;
+}
+
 /* projection onto [lb, ub] that keeps a NaN a NaN (fmin/fmax would replace it by a bound) */
 static double proj(double v, double lb, double ub) { return v < lb ? lb : (v > ub ? ub : v); }
 
@@ -791,6 +800,10 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
              * and the test allows 1e-13 |phi| of roundoff in the merit sum */
             double noise = 1.0 + fabs(phi0);
             if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) { accepted = 1; break; }
+            /* first iteration: IPOPT's filter acceptance (Waechter & Biegler 2006, eqs. (18)-(21)) -- its filter then
+             * holds only theta_max = 1e4 max(1, theta_0), the cold start is far from feasible (no switching), so a
+             * trial is taken when it reduces the constraint violation or the objective sufficiently */
+            if (it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct)) { accepted = 1; break; }
             alpha *= 0.5;
         }
         if (!accepted) { status = ORACLE_LINESEARCH_FAILED; break; }

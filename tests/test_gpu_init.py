@@ -44,12 +44,14 @@ def test_init_hold_matches_oracle(kkt, bounds, model_json, mmpc_mod, oracle):
     assert np.abs(g["V"] - ref["V"]).max() / np.abs(ref["V"]).max() < 1e-7
 
 
-def test_init_hold_cuts_the_tail(model_json, mmpc_mod, oracle):
+def test_init_hold_same_point_no_longer_tail(model_json, mmpc_mod, oracle):
     N, h, B = 30, 0.002, 4096
     x0, up, tr = oracle.synth(20250213, 0, B, N, h)
     w = np.array(WEIGHTS_CFG)
     a = mmpc_mod.Solver(model_json(N=N)).solve_batch_host(x0, up, tr, w)
     b = mmpc_mod.Solver(model_json(N=N, name="hold"), init_states=mmpc_mod.INIT_HOLD_X0).solve_batch_host(x0, up, tr, w)
     assert (a["status"] == 0).all() and (b["status"] == 0).all()
-    assert b["iters"].max() < a["iters"].max() and b["iters"].mean() < a["iters"].mean()
+    # with the exact Hessian and IPOPT's first-iteration acceptance both start-ups need at most 4 iterations at cfg#2
+    # (Gauss-Newton from V = 0 needed 9): the held start no longer shortens the tail, and must not lengthen it
+    assert b["iters"].max() <= a["iters"].max() and b["iters"].mean() <= a["iters"].mean() + 0.25
     assert np.abs(a["V"] - b["V"]).max() / np.abs(a["V"]).max() < 1e-7
