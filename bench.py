@@ -77,8 +77,9 @@ def parse(argv=None):
                     help="outer tolerance: tol_grad = tol, tol_defect = tol/100 (default: 1e-8 / 1e-10)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--init", choices=["as_given", "hold_x0"], default="as_given",
-                    help="mmpc_opts.init_states: the reference's cold start (V = 0) or x_1..x_N = x_0 (DESIGN 3d)")
+    ap.add_argument("--init", choices=["zero", "as_given", "hold_x0"], default="zero",
+                    help="mmpc_opts.init_states: the reference's cold start V = 0 (zero: MMPC_INIT_ZERO, V not read; "
+                         "as_given: V zeroed every step), or x_1..x_N = x_0 (DESIGN 3d)")
     ap.add_argument("--hessian", choices=["auto", "gauss_newton", "exact"], default="auto",
                     help="mmpc_opts.hessian: AUTO = exact Lagrangian Hessian where supported (DESIGN.md 3e)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
@@ -186,7 +187,8 @@ class _StandInSolver:
         V[:, self.nx:self.nx + self.nu] = x0[:, :self.nu]
         st.zero_()
         it.fill_(1)
-        kkt.zero_()
+        if kkt is not None:
+            kkt.zero_()
 
 
 # ------------------------------------------------------------------ one rank
@@ -225,7 +227,8 @@ def run_rank(args):
         ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt]
         solver = mmpc.Solver(path, device=local, kkt_solver=ksolver, factor_fp32=cfg["fp32"],
                              tol_grad=tol_grad, tol_defect=tol_defect,
-                             init_states=mmpc.INIT_HOLD_X0 if args.init == "hold_x0" else mmpc.INIT_AS_GIVEN,
+                             init_states={"zero": mmpc.INIT_ZERO, "as_given": mmpc.INIT_AS_GIVEN,
+                                          "hold_x0": mmpc.INIT_HOLD_X0}[args.init],
                              hessian={"auto": mmpc.HESSIAN_AUTO, "gauss_newton": mmpc.HESSIAN_GAUSS_NEWTON,
                                       "exact": mmpc.HESSIAN_EXACT}[args.hessian])
         solver.reserve_workspace(B)
@@ -239,33 +242,37 @@ def run_rank(args):
     tr = torch.empty((B, N, nx), **f64)
     w = torch.tensor(cfg["weights"], **f64)
     V = torch.zeros((B, NV), **f64)
-    st = torch.empty(B, dtype=torch.int32, device=dev)
-    it = torch.empty(B, dtype=torch.int32, device=dev)
-    kkt = torch.empty(B, **f64)
+    # results the reference consumes per tick: u_0* (ModelControl.cpp:174-190), status, iterations -- one byte
+    # buffer per rank, [B][nu] f64 u_0* | [B] i32 status | [B] i32 iterations; the solve writes status and
+    # iterations straight into it, u_0* is one strided copy out of V, and the buffer goes to rank 0's host in one
+    # D2H (N > 1: one all_gather_into_tensor over RCCL first)
+    nbytes = B * (8 * nu + 8)
+    res = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    u0 = res[:B * nu * 8].view(torch.float64).view(B, nu)
+    st = res[B * nu * 8:B * nu * 8 + 4 * B].view(torch.int32)
+    it = res[B * nu * 8 + 4 * B:].view(torch.int32)
     sh = stream.cuda_stream if stream is not None else None
     first, _ = mdist.shard(B, rank)
     solver.synth(SEED, first, B, x0, up, tr, stream=sh)
     mdist.broadcast_shared(w)   # shared weights from rank 0 (identical here by construction)
 
-    # results the reference consumes per tick: u_0* (ModelControl.cpp:174-190), status, iterations
-    ncol = nu + 2
-    pack = torch.empty((B, ncol), **f64)
-    table = torch.empty((world * B, ncol), **f64) if world > 1 else pack
+    table = torch.empty(world * nbytes, dtype=torch.uint8, device=dev) if world > 1 else res
     pin = dict(pin_memory=True) if not standin else {}
-    host = [torch.empty((world * B, ncol), dtype=torch.float64, **pin) for _ in range(2)]
+    host = [torch.empty(world * nbytes, dtype=torch.uint8, **pin) for _ in range(2)]
+    # MMPC_INIT_ZERO: the cold start V = 0 without reading V (no per-step memset); as_given zeroes V each step
+    zero_v = args.init == "as_given" or standin
 
     def results_to_host(k):
-        pack[:, :nu] = V[:, nx:nx + nu]
-        pack[:, nu] = st
-        pack[:, nu + 1] = it
+        u0.copy_(V[:, nx:nx + nu])
         if world > 1:   # N > 1: one all_gather_into_tensor (RCCL over xGMI) to rank 0's device, then D2H there
-            dist.all_gather_into_tensor(table, pack, async_op=True).wait()   # stream-ordered on GPUs
+            dist.all_gather_into_tensor(table, res, async_op=True).wait()   # stream-ordered on GPUs
         if rank == 0:
             host[k % 2].copy_(table, non_blocking=not standin)
 
     def solve():
-        V.zero_()   # cold start (reference first call: v_init = 0, ModelControl.cpp:29-50)
-        solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=sh)
+        if zero_v:
+            V.zero_()   # cold start (reference first call: v_init = 0, ModelControl.cpp:29-50)
+        solver.solve_batch(B, x0, up, tr, w, V, st, it, None, stream=sh)
 
     for k in range(args.warmup):
         solve()
@@ -280,9 +287,10 @@ def run_rank(args):
     t0 = time.perf_counter()
     for k in range(args.steps):
         if ev:
-            V.zero_()
+            if zero_v:
+                V.zero_()
             ev[k][0].record(stream)
-            solver.solve_batch(B, x0, up, tr, w, V, st, it, kkt, stream=sh)
+            solver.solve_batch(B, x0, up, tr, w, V, st, it, None, stream=sh)
             ev[k][1].record(stream)
         else:
             solve()
@@ -297,18 +305,19 @@ def run_rank(args):
     iters = it.cpu().numpy()
     status = st.cpu().numpy()
     # rank 0's host table of the last step against every rank's own results
-    mine = pack.cpu()
+    mine = res.cpu()
     ok = True
     if rank == 0:
         last = host[(args.steps - 1) % 2]
-        ok = bool(torch.equal(last[:B], mine))
-        conv = int((last[:, nu] == 0).sum().item())
+        ok = bool(torch.equal(last[:nbytes], mine))
+        conv = sum(int((last[r * nbytes + B * nu * 8:r * nbytes + B * nu * 8 + 4 * B].view(torch.int32) == 0).sum())
+                   for r in range(world))
         tail = last
     else:
         conv = 0
         tail = None
     if world > 1:
-        ok = bool(torch.equal(table[rank * B:(rank + 1) * B].cpu(), mine)) and ok
+        ok = bool(torch.equal(table[rank * nbytes:(rank + 1) * nbytes].cpu(), mine)) and ok
         ok = mdist.sum_over_ranks(int(not ok), device=dev if not standin else None) == 0
     total = B * world * args.steps
     value = total / elapsed
@@ -331,8 +340,9 @@ def run_rank(args):
                    "kkt_solver": {0: "stand-in (test)", 1: "condensed (wave per instance)",
                                   2: "riccati (lane per instance)", 3: "riccati (16 lanes per instance)"}[ksolver],
                    "hessian": {1: "gauss-newton", 2: "exact (Lagrangian, IPOPT's default)"}[hess],
-                   "init_states": "V as given (reference cold start V = 0)" if args.init == "as_given"
-                   else "x_1..x_N = x_0 (MMPC_INIT_HOLD_X0)",
+                   "init_states": {"zero": "reference cold start V = 0 (MMPC_INIT_ZERO: V not read)",
+                                   "as_given": "reference cold start V = 0 (V zeroed every step)",
+                                   "hold_x0": "x_1..x_N = x_0 (MMPC_INIT_HOLD_X0)"}[args.init],
                    "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) gathered to "
                                    "rank 0 by RCCL all_gather_into_tensor, then D2H into pinned memory"
                                    if world > 1 else "batch-shard x1; per-step results D2H into pinned memory"),
@@ -344,8 +354,10 @@ def run_rank(args):
     }
     if standin:
         out["standin"] = True
-        if tail is not None:
-            out["standin_u0_first_col"] = tail[:, 0].tolist()
+        if tail is not None:   # u_0*[:, 0] of every rank's slice of the gathered table
+            out["standin_u0_first_col"] = [v for r in range(world)
+                                           for v in tail[r * nbytes:r * nbytes + B * nu * 8].view(torch.float64)
+                                           .view(B, nu)[:, 0].tolist()]
     else:
         import mmpc
         out["kernel_ms"] = kern_ms

@@ -110,8 +110,11 @@ enum mmpc_kkt_solver {
 enum mmpc_init_states {
     MMPC_INIT_AS_GIVEN = 0, /* the reference: V as given (first call zeros, ModelControl.cpp:29-50; later the
                                previous solution, :160-161), x_0 pinned to the measured state */
-    MMPC_INIT_HOLD_X0 = 1   /* x_1..x_N start at the measured state x_0 (controls as given): a consistent-ish
+    MMPC_INIT_HOLD_X0 = 1,  /* x_1..x_N start at the measured state x_0 (controls as given): a consistent-ish
                                state trajectory for cold starts, fewer SQP iterations */
+    MMPC_INIT_ZERO = 2      /* the reference's first call, V = 0 with x_0 pinned (ModelControl.cpp:29-50), without
+                               reading V_inout: a cold start needs no zeroed input (same iterates as AS_GIVEN on a
+                               zero V) */
 };
 
 /* Hessian of each SQP subproblem.  The reference's IPOPT uses the exact Lagrangian Hessian by default

@@ -197,7 +197,7 @@ int validate_opts(const mmpc_opts* o) {
     if (o->kkt_solver < MMPC_KKT_AUTO || o->kkt_solver > MMPC_KKT_RICCATI_GROUP)
         return fail(MMPC_ERR_INVALID_ARG, "unknown kkt_solver");
     if (o->factor_fp32 != 0 && o->factor_fp32 != 1) return fail(MMPC_ERR_INVALID_ARG, "factor_fp32 must be 0 or 1");
-    if (o->init_states != MMPC_INIT_AS_GIVEN && o->init_states != MMPC_INIT_HOLD_X0)
+    if (o->init_states != MMPC_INIT_AS_GIVEN && o->init_states != MMPC_INIT_HOLD_X0 && o->init_states != MMPC_INIT_ZERO)
         return fail(MMPC_ERR_INVALID_ARG, "unknown init_states");
     if (o->hessian < MMPC_HESSIAN_AUTO || o->hessian > MMPC_HESSIAN_EXACT)
         return fail(MMPC_ERR_INVALID_ARG, "unknown hessian");
@@ -715,6 +715,7 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.kkt = kkt;
     p.trace = trace;
     p.init_hold = h->opts.init_states == MMPC_INIT_HOLD_X0;
+    p.init_zero = h->opts.init_states == MMPC_INIT_ZERO;
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
     // points pass NULL for bounds that are all infinite
     const bool bounded = u_lb || u_ub;

@@ -221,11 +221,14 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         const double* Vin = p.V + ii * (int64_t)NV;
         for (int k = gl; k <= N; k += G) {
 #pragma unroll
-            for (int r = 0; r < NX; ++r) sX[k * NX + r] = (k == 0 || p.init_hold) ? p.x0[ii * NX + r] : Vin[k * ND + r];
+            for (int r = 0; r < NX; ++r)
+                sX[k * NX + r] = (k == 0 || p.init_hold) ? p.x0[ii * NX + r] : (p.init_zero ? 0.0 : Vin[k * ND + r]);
             if (k < N) {
 #pragma unroll
-                for (int c = 0; c < NU; ++c)
-                    sU[k * NU + c] = BOUNDED ? proj(Vin[k * ND + NX + c], lbv[c], ubv[c]) : Vin[k * ND + NX + c];
+                for (int c = 0; c < NU; ++c) {
+                    const double v = p.init_zero ? 0.0 : Vin[k * ND + NX + c];
+                    sU[k * NU + c] = BOUNDED ? proj(v, lbv[c], ubv[c]) : v;
+                }
 #pragma unroll
                 for (int r = 0; r < NX; ++r) sR[k * NX + r] = trg[k * NX + r];
             }

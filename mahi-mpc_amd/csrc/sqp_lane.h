@@ -191,13 +191,17 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         const double* Vin = p.V + inst * (int64_t)NV;
         for (int k = 0; k < N; ++k) {
 #pragma unroll
-            for (int r = 0; r < NX; ++r) ST(k, SF::X, r) = (k == 0 || p.init_hold) ? p.x0[inst * NX + r] : Vin[k * ND + r];
+            for (int r = 0; r < NX; ++r)
+                ST(k, SF::X, r) = (k == 0 || p.init_hold) ? p.x0[inst * NX + r] : (p.init_zero ? 0.0 : Vin[k * ND + r]);
 #pragma unroll
-            for (int c = 0; c < NU; ++c)
-                ST(k, SF::U, c) = BOUNDED ? proj(Vin[k * ND + NX + c], lbv[c], ubv[c]) : Vin[k * ND + NX + c];
+            for (int c = 0; c < NU; ++c) {
+                const double v = p.init_zero ? 0.0 : Vin[k * ND + NX + c];
+                ST(k, SF::U, c) = BOUNDED ? proj(v, lbv[c], ubv[c]) : v;
+            }
         }
 #pragma unroll
-        for (int r = 0; r < NX; ++r) ST(N, SF::X, r) = p.init_hold ? p.x0[inst * NX + r] : Vin[N * ND + r];
+        for (int r = 0; r < NX; ++r)
+            ST(N, SF::X, r) = p.init_hold ? p.x0[inst * NX + r] : (p.init_zero ? 0.0 : Vin[N * ND + r]);
         const double* tr = p.traj + inst * (int64_t)N * NX;
         for (int k = 0; k < N; ++k)
 #pragma unroll

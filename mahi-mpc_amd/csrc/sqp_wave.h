@@ -57,6 +57,7 @@ struct SolveParams {
     double* kkt;
     double* trace;  // debug: [B][max_iter+1][8] per-iteration diagnostics, or nullptr
     int init_hold;  // mmpc_opts.init_states == MMPC_INIT_HOLD_X0: x_1..x_N start at x_0 (controls as given)
+    int init_zero;  // mmpc_opts.init_states == MMPC_INIT_ZERO: V is not read, the iterate starts at 0 (x_0 pinned)
 };
 
 enum {
@@ -332,7 +333,7 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
     const double* Vin = p.V + inst * (int64_t)NV;
     for (int i = lane; i < NV; i += 64) {
         const int k = i / ND, r = i - k * ND;
-        const double v = Vin[i];
+        const double v = p.init_zero ? 0.0 : Vin[i];
         const double xv = (p.init_hold && r < NX) ? p.x0[inst * NX + r] : v;  // state entries only
         if (k < N) {
             if (r < NX) sX[k * NX + r] = xv;

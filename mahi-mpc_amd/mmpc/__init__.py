@@ -40,7 +40,7 @@ class MmpcError(RuntimeError):
 
 
 KKT_AUTO, KKT_CONDENSED, KKT_RICCATI, KKT_RICCATI_GROUP = 0, 1, 2, 3
-INIT_AS_GIVEN, INIT_HOLD_X0 = 0, 1
+INIT_AS_GIVEN, INIT_HOLD_X0, INIT_ZERO = 0, 1, 2
 HESSIAN_AUTO, HESSIAN_GAUSS_NEWTON, HESSIAN_EXACT = 0, 1, 2
 MODEL_TWO_LINK_ARM, MODEL_EXO_ARM, MODEL_USER = 0, 1, 2
 USER_LIB_DIR = os.path.join(ROOT, "lib", "user")

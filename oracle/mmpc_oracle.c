@@ -38,7 +38,8 @@ static _Thread_local int t_model = ORACLE_MODEL_TWO_LINK_ARM, t_nx = 4, t_nu = 2
 static oracle_user_jac_fn g_user_jac = NULL;
 /* mmpc_opts.init_states (process-wide): 1 = x_1..x_N start at x_0 */
 static int g_init_hold = 0;
-void oracle_set_init_states(int mode) { g_init_hold = mode == 1; }
+static int g_init_zero = 0;
+void oracle_set_init_states(int mode) { g_init_hold = mode == 1; g_init_zero = mode == 2; }
 static int g_user_nx = 0, g_user_nu = 0;
 static int set_model(int model) {
     if (model == ORACLE_MODEL_TWO_LINK_ARM) { t_model = model; t_nx = 4; t_nu = 2; return 0; }
@@ -554,6 +555,10 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         memcpy(s->U + k * NU, V + k * ND + NX, sizeof(double) * NU);
     }
     memcpy(s->X + N * NX, V + N * ND, sizeof(double) * NX);
+    if (g_init_zero) {  /* MMPC_INIT_ZERO: the reference's first call, V = 0 (ModelControl.cpp:29-50) */
+        memset(s->X, 0, sizeof(double) * (N + 1) * NX);
+        memset(s->U, 0, sizeof(double) * N * NU);
+    }
     memcpy(s->X, x0, sizeof(double) * NX);
     if (g_init_hold)  /* MMPC_INIT_HOLD_X0: the state trajectory starts at the measured state */
         for (int k = 1; k <= N; ++k) memcpy(s->X + k * NX, x0, sizeof(double) * NX);
@@ -898,6 +903,10 @@ static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_pre
         memcpy(s->U + k * NU, V + k * ND + NX, sizeof(double) * NU);
     }
     memcpy(s->X + N * NX, V + N * ND, sizeof(double) * NX);
+    if (g_init_zero) {  /* MMPC_INIT_ZERO: the reference's first call, V = 0 (ModelControl.cpp:29-50) */
+        memset(s->X, 0, sizeof(double) * (N + 1) * NX);
+        memset(s->U, 0, sizeof(double) * N * NU);
+    }
     memcpy(s->X, x0, sizeof(double) * NX);
     if (g_init_hold)  /* MMPC_INIT_HOLD_X0: the state trajectory starts at the measured state */
         for (int k = 1; k <= N; ++k) memcpy(s->X + k * NX, x0, sizeof(double) * NX);

@@ -112,7 +112,8 @@ int oracle_solve_batch_xb(int model, int is_linear, int N, double h, int64_t B, 
                           int max_iter, double tol_grad, double tol_defect, double* V, int32_t* status,
                           int32_t* iters, double* kkt, double* Jout, int nthreads);
 
-/* mmpc_opts.init_states for the following solves (process-wide): 0 = V as given, 1 = x_1..x_N start at x_0 */
+/* mmpc_opts.init_states for the following solves (process-wide): 0 = V as given, 1 = x_1..x_N start at x_0,
+ * 2 = V taken as zero (MMPC_INIT_ZERO) */
 void oracle_set_init_states(int mode);
 
 /* counter-based synthetic cfg#2 instances: splitmix64(seed, index) */

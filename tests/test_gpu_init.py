@@ -55,3 +55,20 @@ def test_init_hold_same_point_no_longer_tail(model_json, mmpc_mod, oracle):
     # (Gauss-Newton from V = 0 needed 9): the held start no longer shortens the tail, and must not lengthen it
     assert b["iters"].max() <= a["iters"].max() and b["iters"].mean() <= a["iters"].mean() + 0.25
     assert np.abs(a["V"] - b["V"]).max() / np.abs(a["V"]).max() < 1e-7
+
+
+@pytest.mark.parametrize("kkt", ["condensed", "group", "lane"])
+def test_init_zero_ignores_V(kkt, model_json, mmpc_mod, oracle):
+    """MMPC_INIT_ZERO: the reference's first call (V = 0, x_0 pinned) without reading V_inout -- garbage in V gives the
+    same solve, bit for bit, as MMPC_INIT_AS_GIVEN on a zeroed V; the oracle agrees."""
+    ks = {"condensed": mmpc_mod.KKT_CONDENSED, "group": mmpc_mod.KKT_RICCATI_GROUP, "lane": mmpc_mod.KKT_RICCATI}[kkt]
+    N, h, B = 30, 0.002, 128
+    x0, up, tr = oracle.synth(20250213, 0, B, N, h)
+    w = np.array(WEIGHTS_CFG)
+    a = mmpc_mod.Solver(model_json(N=N), kkt_solver=ks).solve_batch_host(x0, up, tr, w)
+    s = mmpc_mod.Solver(model_json(N=N, name="z"), kkt_solver=ks, init_states=mmpc_mod.INIT_ZERO)
+    b = s.solve_batch_host(x0, up, tr, w, V=np.full((B, s.NV), np.nan))
+    for k in ("V", "status", "iters", "kkt"):
+        np.testing.assert_array_equal(a[k], b[k])
+    o = oracle.solve_batch(N, h, x0, up, tr, w, V=np.full((B, s.NV), 7.0), init_states=2, solver=s)
+    assert np.abs(o["V"] - b["V"]).max() <= 1e-10 * np.abs(o["V"]).max()
