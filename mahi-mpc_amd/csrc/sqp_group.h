@@ -807,24 +807,30 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             }
             const double Rmr = lu ? w[NX + NU + ru] : 0.0;   // Rm of this lane's u row
             const double upr = p.u_prev[ii * NU + ru];
+            const double lum = lu ? 1.0 : 0.0;
             double unx = 0.0;                                  // u_{k+1}[ru]
             // stage operands (loaded one stage ahead): column r of A's a-rows, column ru of hFu, u_k[ru],
             // u_{k-1}[ru], Q (d_k + x_k - r_{k-1})[r]
-            double nacol[NA], nhfu[NA], nuk, num, nqe;
-            auto load = [&](int k) {
+            double nacol[NA], nhfu[NA], nuk, num, nqe = 0.0;
+            auto load = [&](int k, auto zero_c) {   // zero_c: k == 0 (u_{-1} = u_prev, no Q e_{-1})
+                constexpr bool ZERO = decltype(zero_c)::value;
                 load_acol(k, nacol);
 #pragma unroll
                 for (int s2 = 0; s2 < NA; ++s2) nhfu[s2] = sFu[k * FU + s2 * NU + ru];
                 nuk = sU[k * NU + ru];
-                const double ump = sU[(k > 0 ? k - 1 : 0) * NU + ru];
-                num = k == 0 ? upr : ump;
-                const int km = k > 0 ? k - 1 : 0;
-                const double xk = sX[k * NX + rx], trm = tr[km * NX + rx], dk = sD[k * NX + rx];
-                nqe = Qr * (dk + (xk - trm));
+                if constexpr (ZERO) {
+                    num = upr;
+                } else {
+                    num = sU[(k - 1) * NU + ru];
+                    const double xk = sX[k * NX + rx], trm = tr[(k - 1) * NX + rx], dk = sD[k * NX + rx];
+                    nqe = Qr * (dk + (xk - trm));
+                }
             };
-            load(N - 1);
-#pragma unroll 2
-            for (int k = N - 1; k >= 0; --k) {
+            // stage k: FIRST = (k == N - 1, no u_{k+1}), LAST = (k == 0, no lam_k); peeled so that the inner
+            // stages carry no k-dependent selects or branches
+            auto stage = [&](int k, auto first_c, auto last_c, auto next0_c) {   // NEXT0: k == 1
+                constexpr bool FIRST = decltype(first_c)::value, LAST = decltype(last_c)::value;
+                constexpr bool NEXT0 = decltype(next0_c)::value;
                 double acol[NA], hfu[NA];
 #pragma unroll
                 for (int s2 = 0; s2 < NA; ++s2) {
@@ -832,20 +838,18 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     hfu[s2] = nhfu[s2];
                 }
                 const double uk = nuk, um = num, qe = nqe;
-                load(k > 0 ? k - 1 : 0);
+                if constexpr (!LAST) load(k - 1, std::integral_constant<bool, NEXT0>{});
                 double lamb[NX];
                 sfor<0, NX>([&](auto I) { lamb[I] = row_bcast<I>(lamr); });
                 double g = 0.0;
 #pragma unroll
                 for (int s2 = 0; s2 < NA; ++s2) g = fma(hfu[s2], lamb[NQ + s2], g);
                 g = fma(Rr, uk - um, fma(Rmr, uk, g));
-                if (k + 1 < N) g -= Rr * (unx - uk);
+                if constexpr (!FIRST) g -= Rr * (unx - uk);
                 unx = uk;
-                if (lu) {
-                    gmax = fmax(gmax, fabs(2.0 * g));
-                    nonfinite |= !isfinite(g);
-                }
-                if (k >= 1) {   // (A^T lam)[r] + Q e_{k-1}[r], two partial sums
+                gmax = fmax(gmax, lum * fabs(2.0 * g));   // u-lanes only (0 elsewhere)
+                nonfinite |= lu && !isfinite(g);
+                if constexpr (!LAST) {   // (A^T lam)[r] + Q e_{k-1}[r], two partial sums
                     double t0 = lx ? lamr + qe : 0.0, t1 = 0.0;
 #pragma unroll
                     for (int z = 0; z < NQ; ++z) t1 = fma(hq[z], lamb[z], t1);
@@ -858,9 +862,24 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     lmax = fmax(lmax, fabs(lamr));
                     if (EXACT && lx) sD[k * NX + rx] = lamr;
                 }
+            };
+            using T_ = std::true_type;
+            using F_ = std::false_type;
+            if (N == 1) {
+                load(0, T_{});
+                stage(0, T_{}, T_{}, F_{});
+                return;
             }
+            load(N - 1, F_{});
+            if (N == 2) {
+                stage(1, T_{}, F_{}, T_{});
+            } else {
+                stage(N - 1, T_{}, F_{}, F_{});
+                for (int k = N - 2; k >= 2; --k) stage(k, F_{}, F_{}, F_{});
+                stage(1, F_{}, F_{}, T_{});
+            }
+            stage(0, F_{}, T_{}, F_{});
         };
-        // useW (EXACT): the stage Hessians W_k of wH enter P~ (x-x block), H_ww (u-u) and H_wx (u-x)
         auto backward_dist = [&](bool useW) {
             double Prow[NS], pvr;
             const double lxm = lx ? 1.0 : 0.0;
@@ -876,7 +895,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             for (int j = 0; j < NS; ++j) Prow[j] = j < NX ? qoh[j] : 0.0;   // P~_N = blkdiag(Q, 0)
             pvr = Qr * (lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0);   // Q (x_N - r_{N-1})
             // (the sweep is issue-bound: its LDS operands are read in place; a prefetch buffer spills to AGPRs)
-            for (int k = N - 1; k >= 0; --k) {
+            // stage k; LAST = (k == 0), peeled so that the stages k >= 1 carry no k == 0 selects or branches
+            auto stage = [&](int k, auto last_c) {
+                constexpr bool LAST = decltype(last_c)::value;
                 double hFq[SQ], hFqd[FD], hFu[FU], cc[NX], u[NU], um[NU], acol[NA];
 #pragma unroll
                 for (int i = 0; i < FQ; ++i) hFq[i] = sFq[k * FQ + i];
@@ -886,24 +907,25 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 for (int i = 0; i < FU; ++i) hFu[i] = sFu[k * FU + i];
 #pragma unroll
                 for (int q = 0; q < NX; ++q) cc[q] = sC[k * NX + q];
-                const int km = k >= 1 ? k - 1 : 0;
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
                     u[c] = sU[k * NU + c];
-                    const double v = sU[km * NU + c];
-                    um[c] = (k == 0) ? up[c] : v;
+                    um[c] = LAST ? up[c] : sU[(k - 1) * NU + c];
                 }
                 load_acol(k, acol);
-                const double xk = sX[k * NX + rx], trm = tr[km * NX + rx];
-                const double exr = lx ? xk - trm : 0.0;
-                const double duu = sU[k * NU + ru] - sU[km * NU + ru];
+                double exr = 0.0, duu = 0.0;
+                if constexpr (!LAST) {
+                    const double xk = sX[k * NX + rx], trm = tr[(k - 1) * NX + rx];
+                    exr = lx ? xk - trm : 0.0;
+                    duu = sU[k * NU + ru] - sU[(k - 1) * NU + ru];
+                }
                 double wr[KZ], wu[NU * NU];
                 if constexpr (EXACT) {
 #pragma unroll
                     for (int j = 0; j < KZ; ++j) wr[j] = useW ? nwr[j] : 0.0;
 #pragma unroll
                     for (int j = 0; j < NU * NU; ++j) wu[j] = useW ? nwu[j] : 0.0;
-                    if (useW) load_w(k > 0 ? k - 1 : 0);
+                    if (!LAST && useW) load_w(k - 1);
                 }
                 // T = P~ [B; I] (row r), mv = P~_x. c + p~ (row r)
                 double T[NU], mv = pvr;
@@ -1022,7 +1044,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                     for (int a = 0; a < NU; ++a) wK[(k * NU + a) * (NS + 1) + r] = -(r < NS ? Kcol[a] : kff[a]);
                 }
-                if (k == 0) break;
+                if constexpr (LAST) return;
                 // A^T P_xx A (row r) from the broadcast P_xx, p~_x = A^T mv + Q (x_k - r_{k-1})
                 double Pb[NX][NX];
                 sfor<0, NX>([&](auto I) {
@@ -1064,7 +1086,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                 for (int a = 0; a < NU; ++a) pv2 = fma(-Ycol[a], kff[a], pv2);
                 pvr = pv2;
-            }
+            };
+            for (int k = N - 1; k >= 1; --k) stage(k, std::false_type{});
+            stage(0, std::true_type{});
         };
         if constexpr (DIST) {
             d_recursion_dist();

@@ -154,9 +154,11 @@ struct CodeBlock {
     std::vector<std::string> values;  // one C expression per requested output
     int n_ops = 0;                    // arithmetic/elementary operations emitted
 };
-// inputs: symbol node -> C lvalue text (e.g. "x[2]"); throws if an expression uses an unmapped symbol
+// inputs: symbol node -> C lvalue text (e.g. "x[2]"); throws if an expression uses an unmapped symbol.
+// reciprocal_divisors: quotients sharing a divisor multiply by its reciprocal, computed once (within 1.5 ulp).
 CodeBlock emit_code(const std::vector<sx::NodeP>& outputs, const std::map<const sx::Node*, std::string>& inputs,
-                    const std::string& tmp_prefix = "t", const std::string& indent = "    ");
+                    const std::string& tmp_prefix = "t", const std::string& indent = "    ",
+                    bool reciprocal_divisors = false);
 
 class Function {
 public:

@@ -494,13 +494,21 @@ std::string expr_text(Op op, const std::string& a, const std::string& b) {
 }  // namespace
 
 CodeBlock emit_code(const std::vector<NodeP>& outputs, const std::map<const sx::Node*, std::string>& inputs,
-                    const std::string& tmp_prefix, const std::string& indent) {
+                    const std::string& tmp_prefix, const std::string& indent, bool reciprocal_divisors) {
     CodeBlock cb;
     std::ostringstream body;
     std::unordered_map<const sx::Node*, std::string> text;  // node -> operand text
     std::map<std::tuple<int, std::string, std::string>, std::string> cse;
     int ntmp = 0;
-    for (const sx::Node* n : sx::topo_order(outputs)) {
+    const std::vector<const sx::Node*> order = sx::topo_order(outputs);
+    // reciprocal_divisors: a divisor shared by several quotients is inverted once (1 ulp per quotient; an fp64
+    // division is ~10 GPU instructions, a multiply one)
+    std::unordered_map<const sx::Node*, int> ndiv;
+    std::unordered_map<const sx::Node*, std::string> recip;
+    if (reciprocal_divisors)
+        for (const sx::Node* n : order)
+            if (n->op == Op::Div) ++ndiv[n->b.get()];
+    for (const sx::Node* n : order) {
         if (n->op == Op::Const) {
             text[n] = literal(n->val);
             continue;
@@ -512,15 +520,27 @@ CodeBlock emit_code(const std::vector<NodeP>& outputs, const std::map<const sx::
             continue;
         }
         std::string a = text.at(n->a.get()), b = n->b ? text.at(n->b.get()) : std::string();
-        if ((n->op == Op::Add || n->op == Op::Mul) && b < a) std::swap(a, b);  // commutative: canonical order
-        const auto key = std::make_tuple(static_cast<int>(n->op), a, b);
+        Op op = n->op;
+        if (op == Op::Div && reciprocal_divisors && ndiv[n->b.get()] >= 2) {
+            auto r = recip.find(n->b.get());
+            if (r == recip.end()) {
+                const std::string t = tmp_prefix + std::to_string(ntmp++);
+                body << indent << "const double " << t << " = 1.0 / " << b << ";\n";
+                ++cb.n_ops;
+                r = recip.emplace(n->b.get(), t).first;
+            }
+            op = Op::Mul;
+            b = r->second;
+        }
+        if ((op == Op::Add || op == Op::Mul) && b < a) std::swap(a, b);  // commutative: canonical order
+        const auto key = std::make_tuple(static_cast<int>(op), a, b);
         auto it = cse.find(key);
         if (it != cse.end()) {
             text[n] = it->second;
             continue;
         }
         const std::string t = tmp_prefix + std::to_string(ntmp++);
-        body << indent << "const double " << t << " = " << expr_text(n->op, a, b) << ";\n";
+        body << indent << "const double " << t << " = " << expr_text(op, a, b) << ";\n";
         ++cb.n_ops;
         cse[key] = t;
         text[n] = t;
