@@ -2,57 +2,55 @@
 //
 // The reference takes f as a casadi::SX expression supplied by the caller of
 // ModelGenerator (include/Mahi/Mpc/ModelGenerator.hpp:23) and code-generates it
-// to C (ModelGenerator.cpp:235-259).  Here each model is a device template over
-// the scalar type (double or Dual<NX+NU>), compiled into the solver kernel.
+// to C (ModelGenerator.cpp:235-259).  Here each built-in model is a device struct with closed-form values and
+// derivatives (eval, eval_acc_jac, eval_jac, eval_hess), compiled into the solver kernels; SX-generated models
+// (host/src/ModelGenerator.cpp) emit the same interface.
 #pragma once
 #include <type_traits>
 
-#include "dual.h"
+#include "device.h"
 #include "exo_model_gen.h"
-#include "two_link_hess_gen.h"
+#include "two_link_fast.h"
 
 namespace mmpc {
 
 // 2-link planar arm / double pendulum of examples/ex_model_generate.cpp:24-43
 // (L = m = 1, g = 9.81), state [qA, qB, qA_dot, qB_dot], control [TA, TB].
-// The two accelerations restate :36-37 term by term.
+// Values, Jacobian and the weighted Hessian come from the closed form of two_link_fast.h (one sincos per
+// angle, quotient rule); the oracle restates :36-37 term by term (tests/test_sx_models.py compares the two).
 struct TwoLinkArm {
     static constexpr int NX = 4;
     static constexpr int NU = 2;
-
-    template <class T>
-    MMPC_HD static void xdot(const T* x, const T* u, T* xd) {
-        constexpr double L = 1.0, m = 1.0, g = 9.81;
-        constexpr double LLm = L * L * m, Lgm = L * g * m;
-        const T qA = x[0], qB = x[1], dA = x[2], dB = x[3], TA = u[0], TB = u[1];
-        T sB, cB;
-        mm_sincos(qB, sB, cB);
-        const T cA = mm_cos(qA);
-        const T cAB = mm_cos(qA + qB);
-        const T dA2 = dA * dA, dB2 = dB * dB, dAdB = dA * dB, cBsB = cB * sB;
-        const T inv_den = 1.0 / (LLm * (cB * cB - 2.0));
-        const T nA = TA - TB - TB * cB + LLm * (dA2 * sB) + LLm * (dB2 * sB) - (2.0 * Lgm) * cA
-                     + LLm * (dA2 * cBsB) + (2.0 * LLm) * (dAdB * sB) + Lgm * (cAB * cB);
-        const T nB = TA - 3.0 * TB + TA * cB - 2.0 * (TB * cB) + (2.0 * Lgm) * cAB
-                     + (3.0 * LLm) * (dA2 * sB) + LLm * (dB2 * sB) - (2.0 * Lgm) * cA
-                     + (2.0 * LLm) * (dA2 * cBsB) + LLm * (dB2 * cBsB) - (2.0 * Lgm) * (cA * cB)
-                     + (2.0 * LLm) * (dAdB * sB) + Lgm * (cAB * cB) + (2.0 * LLm) * (dAdB * cBsB);
-        xd[0] = dA;
-        xd[1] = dB;
-        xd[2] = -(nA * inv_den);
-        xd[3] = nB * inv_den;
-    }
     static constexpr int NQ = 2;  // second-order: x = [q; qd], xdot = [qd; acc(x, u)]
-    MMPC_HD static void eval(const double* x, const double* u, double* xd) { xdot<double>(x, u, xd); }
-    MMPC_HD static void eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu);
+    MMPC_HD static void eval(const double* x, const double* u, double* xd) { TwoLinkFast::eval(x, u, xd); }
+    MMPC_HD static void eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
+        double Fq[4], Fqd[4], Fu[4];
+        TwoLinkFast::eval_acc_jac(x, u, xd + 2, Fq, Fqd, Fu);
+        xd[0] = x[2];
+        xd[1] = x[3];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) fx[r * 4 + c] = (c == 2 + r) ? 1.0 : 0.0;
+            fu[r * 2] = fu[r * 2 + 1] = 0.0;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                fx[(2 + r) * 4 + c] = Fq[r * 2 + c];
+                fx[(2 + r) * 4 + 2 + c] = Fqd[r * 2 + c];
+                fu[(2 + r) * 2 + c] = Fu[r * 2 + c];
+            }
+        }
+    }
     // acceleration and its partials d acc/dq [NQ*NQ], d acc/dqd [NQ*NQ], d acc/du [NQ*NU] (row-major)
     MMPC_HD static void eval_acc_jac(const double* x, const double* u, double* acc, double* Fq, double* Fqd,
-                                     double* Fu);
+                                     double* Fu) {
+        TwoLinkFast::eval_acc_jac(x, u, acc, Fq, Fqd, Fu);
+    }
     // W = sum_s lam[s] d^2 acc_s / d(x, u)^2 (6 x 6 row-major): the dynamics part of the Lagrangian Hessian
-    // (CasADi nlp_hess_l, ModelGenerator.cpp:238), symbolic code generated from the SX statement of :36-37
+    // (CasADi nlp_hess_l, ModelGenerator.cpp:238)
     static constexpr bool kHasHess = true;
     MMPC_HD static void eval_hess(const double* x, const double* u, const double* lam, double* W) {
-        TwoLinkArmHess::eval_hess(x, u, lam, W);
+        TwoLinkFast::eval_hess(x, u, lam, W);
     }
 };
 
@@ -65,27 +63,6 @@ template <class M>
 struct HasHess<M, std::enable_if_t<M::kHasHess>> {
     static constexpr bool value = true;
 };
-
-// Forward-mode Jacobian of a model written as a scalar template: values and the continuous-time
-// Jacobians fx[NX*NX], fu[NX*NU] row-major.
-template <class Model>
-MMPC_HD void dual_eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
-    constexpr int NX = Model::NX, NU = Model::NU, K = NX + NU;
-    Dual<K> xv[NX], uv[NU], xdv[NX];
-#pragma unroll
-    for (int i = 0; i < NX; ++i) xv[i] = dual_var<K>(x[i], i);
-#pragma unroll
-    for (int i = 0; i < NU; ++i) uv[i] = dual_var<K>(u[i], NX + i);
-    Model::template xdot<Dual<K>>(xv, uv, xdv);
-#pragma unroll
-    for (int r = 0; r < NX; ++r) {
-        xd[r] = xdv[r].v;
-#pragma unroll
-        for (int c = 0; c < NX; ++c) fx[r * NX + c] = xdv[r].d[c];
-#pragma unroll
-        for (int c = 0; c < NU; ++c) fu[r * NU + c] = xdv[r].d[NX + c];
-    }
-}
 
 // 4-DoF forearm/wrist exo, state [q0..q3, qd0..qd3] (util/testCorrectEquations.py:16-23),
 // control tau[4].  xdot = [qd; M(q)^-1 (tau - D qd - G(q))] with M(q) of src/inverseTest.cpp:59-74
@@ -220,31 +197,6 @@ struct ExoArm {
         }
     }
 };
-
-MMPC_HD void TwoLinkArm::eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
-    dual_eval_jac<TwoLinkArm>(x, u, xd, fx, fu);
-}
-MMPC_HD void TwoLinkArm::eval_acc_jac(const double* x, const double* u, double* acc, double* Fq, double* Fqd,
-                                      double* Fu) {
-    constexpr int K = NX + NU;
-    Dual<K> xv[NX], uv[NU], xdv[NX];
-#pragma unroll
-    for (int i = 0; i < NX; ++i) xv[i] = dual_var<K>(x[i], i);
-#pragma unroll
-    for (int i = 0; i < NU; ++i) uv[i] = dual_var<K>(u[i], NX + i);
-    xdot<Dual<K>>(xv, uv, xdv);
-#pragma unroll
-    for (int r = 0; r < NQ; ++r) {
-        acc[r] = xdv[NQ + r].v;
-#pragma unroll
-        for (int c = 0; c < NQ; ++c) {
-            Fq[r * NQ + c] = xdv[NQ + r].d[c];
-            Fqd[r * NQ + c] = xdv[NQ + r].d[NQ + c];
-        }
-#pragma unroll
-        for (int c = 0; c < NU; ++c) Fu[r * NU + c] = xdv[NQ + r].d[NX + c];
-    }
-}
 
 // Values and continuous-time Jacobians of any model: fx[NX*NX], fu[NX*NU] row-major.
 template <class Model>
