@@ -20,7 +20,7 @@ the process is a rank itself.
 Prints ONE JSON line on rank 0 (driver contract) with two extra objects:
   roofline      the dominant kernel's achieved FP64 rate (its own algorithmic flop count) vs the MI355X FP64
                 vector peak; kernel time from HIP events on the launch stream;
-  cpu_baseline  the oracle/ CPU restatement (same GN-SQP NLP, fp64) on a bounded sample, rank 0 at N = 1 only,
+  cpu_baseline  the oracle/ CPU restatement (same NLP and SQP, fp64) on a bounded sample, rank 0 at N = 1 only,
                 with its agreement with the GPU solutions and both iteration histograms.
 """
 from __future__ import annotations
@@ -47,7 +47,8 @@ WEIGHTS_EXO = [10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4
 _EXO_METRIC = "MPC solves/sec (whole node), exo nx=8 N=50 batch (SURVEY.md 8d cfg#3/#4)"
 CONFIGS = {
     "cfg2": dict(model="two_link_arm", nx=4, nu=2, N=30, B=4096, weights=WEIGHTS, metric=METRIC, fp32=False,
-                 workload="cfg#2: 2-link arm nx=4 nu=2, N=30, h=2 ms, cold-start GN-SQP to ||grad||<=1e-8, ||g||<=1e-10"),
+                 workload="cfg#2: 2-link arm nx=4 nu=2, N=30, h=2 ms, cold-start SQP (exact or Gauss-Newton Hessian: config.hessian) to "
+                          "||grad||<=1e-8, ||g||<=1e-10"),
     "cfg3": dict(model="exo_arm", nx=8, nu=4, N=50, B=65536, weights=WEIGHTS_EXO, metric=_EXO_METRIC, fp32=False,
                  workload="cfg#3: 4-DoF exo nx=8 nu=4 (build-defined parameters), N=50, h=2 ms, cold-start GN-SQP "
                           "(Riccati KKT) to ||grad||<=1e-8, ||g||<=1e-10"),
@@ -128,7 +129,7 @@ def launch(args, argv) -> int:
 
 # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1 only)
 def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1):
-    """Oracle (oracle/liboracle.so: the same NLP and GN-SQP in plain C + OpenMP, dense condensed KKT) on a
+    """Oracle (oracle/liboracle.so: the same NLP and SQP in plain C + OpenMP, dense condensed KKT) on a
     bounded sample of the same seeded workload, plus its agreement with the GPU on the shared instances."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as o
@@ -156,7 +157,7 @@ def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, he
     hist = lambda a: {int(k): int(v) for k, v in zip(*np.unique(a, return_counts=True))}  # noqa: E731
     return dict(value=n / dt, unit="solves/s", cores=threads, kind="port",
                 sample=f"first {n} {cfg['workload'].split(':')[0]} instances (seed {SEED}), cold start, {dt:.1f} s "
-                       f"wall, {int((r['status'] == 0).sum())}/{n} converged; oracle GN-SQP with a DENSE condensed "
+                       f"wall, {int((r['status'] == 0).sum())}/{n} converged; oracle SQP with a DENSE condensed "
                        f"KKT (Cholesky of the N*nu Hessian, not the Riccati recursion the GPU runs), "
                        f"{'exact' if hessian == 2 else 'Gauss-Newton'} Hessian as the GPU, "
                        f"{threads} OpenMP threads",

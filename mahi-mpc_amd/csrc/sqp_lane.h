@@ -136,8 +136,13 @@ MMPC_HD void at_mul(T h, const T* hFq, const T* hFqd, const T* v, T* out) {
 // Per-lane pointer to stage k of the workspace, opaque to the optimiser: every access of a stage loop is
 // derived from it (offset folded into the instruction or one add), so nothing is hoisted out of the loop.
 // Without it LICM materialises one 64-bit offset per (field, element) before the loop and spills them.
-__device__ __forceinline__ double* stage_ptr(double* wsb, int64_t k, int SS, int lane) {
-    double* q = wsb + k * SS * 64 + lane;
+// The pointer is typed global (address space 1): an opaque generic pointer compiles to flat_load/flat_store,
+// whose every use waits for vmcnt(0) AND lgkmcnt(0) (flat operations complete out of order), i.e. drains the
+// next stage's prefetches and all LDS traffic at each workspace access.
+template <class T>
+using gmem = __attribute__((address_space(1))) T;
+__device__ __forceinline__ gmem<double>* stage_ptr(double* wsb, int64_t k, int SS, int lane) {
+    gmem<double>* q = (gmem<double>*)(wsb + k * SS * 64 + lane);
     asm volatile("" : "+v"(q));
     return q;
 }
@@ -258,7 +263,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 Model::eval(x, u, xd);                                                                   \
             }                                                                                            \
         } else {                                                                                         \
-            double* const lp_ = stage_ptr(wsb, N + 1, SS, lane);                                         \
+            gmem<double>* const lp_ = stage_ptr(wsb, N + 1, SS, lane);                                         \
             double dx_[NX], du_[NU];                                                                     \
             _Pragma("unroll") for (int i_ = 0; i_ < NX; ++i_) dx_[i_] = x[i_] - lp_[((LXS) + (i_)) * 64];        \
             _Pragma("unroll") for (int i_ = 0; i_ < NU; ++i_) du_[i_] = u[i_] - lp_[((LUS) + (i_)) * 64];        \
@@ -319,7 +324,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             }
             #pragma unroll 1
             for (int k = 0; k < N; ++k) {
-                double* const sk = stage_ptr(wsb, k, SS, lane);
+                gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
                 double u[NU], xn[NX], rk[NX], xd[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU];
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
@@ -420,7 +425,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 for (int r = 0; r < NX; ++r) xpf[r] = ST(N - 1, SF::X, r);
                 #pragma unroll 1
                 for (int k = N - 1; k >= 0; --k) {
-                    double* const sk = stage_ptr(wsb, k, SS, lane);
+                    gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
                     double x[NX], u[NU], um[NU], cc[NX], dk[NX], rkm[NX], xd[NX], hFq[SQ], hFqd[NA * NA],
                         hFu[NA * NU], tg[NU];
 #pragma unroll
@@ -585,7 +590,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     // workspace (in registers next to G, Y and the stage blocks it spills).
                     // p~_k x part: A^T mv + Q (x_k - r_{k-1}) (fp64).
                     double pn[NS];
-                    FT* const sw = reinterpret_cast<FT*>(stage_ptr(wsb, kScratch, SS, 0)) + lane;  // per-lane scratch stage
+                    gmem<FT>* const sw = (gmem<FT>*)(stage_ptr(wsb, kScratch, SS, 0)) + lane;  // per-lane scratch stage
                     if (k >= 1) {
                         if constexpr (!WLDS)
 #pragma unroll
@@ -658,8 +663,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                             for (int q = a + 1; q < NU; ++q) t = fma(-(double)Ld[q][a], kh[q], t);
                             kh[a] = t / (double)Ld[a][a];
                         }
-                        double* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
-                        FT* const kk = reinterpret_cast<FT*>(kb + NU * 64) + lane;
+                        gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
+                        gmem<FT>* const kk = (gmem<FT>*)(kb + NU * 64) + lane;
 #pragma unroll
                         for (int a = 0; a < NU; ++a) {
                             kb[a * 64 + lane] = -kh[a];
@@ -825,7 +830,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                 }
                 #pragma unroll 1
                 for (int k = 0; k < N; ++k) {
-                    double* const sk = stage_ptr(wsb, k, SS, lane);
+                    gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
                     double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU], dxk[NX];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) dxk[r] = dx[r];
@@ -842,8 +847,8 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                         upf[c] = SK(1, SF::U, c);  // stage N's U slot exists (unused) when k = N-1
                     }
                     double du[NU];
-                    const double* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
-                    const FT* const kk = reinterpret_cast<const FT*>(kb + NU * 64) + lane;
+                    const gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
+                    const gmem<FT>* const kk = (const gmem<FT>*)(kb + NU * 64) + lane;
 #pragma unroll
                     for (int a = 0; a < NU; ++a) {
                         const int base = a * NS;
@@ -948,7 +953,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
             }
             #pragma unroll 1
             for (int k = 0; k < N; ++k) {
-                double* const sk = stage_ptr(wsb, k, SS, lane);
+                gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
                 double u[NU], xn[NX], xd[NX], rk[NX];
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
@@ -1009,10 +1014,10 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         if constexpr (XB) {  // y and the duals of stage k's (x_{k+1} | u_k), as oracle solve_one_ip
             #pragma unroll 1
             for (int k = 0; k < N; ++k) {
-                double* const sk = stage_ptr(wsb, k, SS, lane);
+                gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
 #pragma unroll
                 for (int j = 0; j < NY; ++j) {
-                    double& y = j < NX ? SK(1, SF::X, j) : SK(0, SF::U, j - NX);
+                    gmem<double>& y = j < NX ? SK(1, SF::X, j) : SK(0, SF::U, j - NX);
                     const double dy = j < NX ? SK(1, SF::DX, j) : SK(0, SF::DU, j - NX);
                     double zl = SK(0, SF::ZL, j), zu = SK(0, SF::ZU, j), yn;
                     ip_update(y, dy, yl[j], yu[j], zl, zu, mub, alpha, az, yn);
@@ -1025,7 +1030,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
         } else {
             #pragma unroll 1
             for (int k = 0; k <= N; ++k) {
-                double* const sk = stage_ptr(wsb, k, SS, lane);
+                gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
                 if (k > 0) {
 #pragma unroll
                     for (int r = 0; r < NX; ++r) SK(0, SF::X, r) = fma(alpha, SK(0, SF::DX, r), SK(0, SF::X, r));

@@ -42,6 +42,23 @@ for b in worst:
 out = dict(rc=rc, hist=hist, mean=float(it.mean()), total_passes=int((it + 1).sum()),
            small_defect_passes=small_c_total, small_defect_not_final=small_c_not_final,
            worst_idx=worst.tolist(), worst_trace_grad_defect_alpha=rows)
+# per final iteration count: quantiles of the stop-test norms at the check before the last one, and how many took
+# a step shorter than alpha = 1
+q = {}
+for n in sorted(set(it.tolist())):
+    sel = it == n
+    if n == 0:
+        continue
+    g, c = T[sel, n - 1, 0], T[sel, n - 1, 1]
+    al = T[sel, :n, 5]
+    q[int(n)] = dict(count=int(sel.sum()),
+                     grad_before_last_q=[float(v) for v in np.quantile(g, [0.0, 0.5, 0.9, 1.0])],
+                     defect_before_last_q=[float(v) for v in np.quantile(c, [0.0, 0.5, 0.9, 1.0])],
+                     short_steps=int((al < 1.0).sum()),
+                     grad_by_iter_median=[float(np.median(T[sel, i, 0])) for i in range(n + 1)],
+                     defect_by_iter_median=[float(np.median(T[sel, i, 1])) for i in range(n + 1)])
+out["by_iters"] = q
 json.dump(out, open("gpurun_out/cfg2_trace.json", "w"), indent=1)
 print(json.dumps({k: out[k] for k in ("rc", "hist", "mean", "total_passes", "small_defect_passes",
                                       "small_defect_not_final")}))
+print(json.dumps(q, indent=1))

@@ -211,9 +211,12 @@ constexpr double kDamping[4] = {{{", ".join(lit(sp.Rational(v)) for v in pj["dam
 // the {len(coefs)} distinct polynomial coefficients
 __constant__ double kCoef[{len(coefs)}] = {{{", ".join(lit(v) for v in coefs)}}};
 
-// table pointer made opaque per call: the loads stay at their uses (no loop-invariant hoisting)
-__device__ __forceinline__ const double* coef_table() {{
-    const double* K = kCoef;
+// table pointer made opaque per call: the loads stay at their uses (no loop-invariant hoisting).  Typed constant
+// (address space 4), so the loads are scalar s_load: an opaque generic pointer becomes flat_load, and every use of
+// a flat load waits for all outstanding vector-memory and LDS operations of the wave.
+using cdouble = __attribute__((address_space(4))) const double;
+__device__ __forceinline__ cdouble* coef_table() {{
+    cdouble* K = (cdouble*)kCoef;
     asm volatile("" : "+s"(K));
     return K;
 }}
@@ -228,7 +231,7 @@ struct TrigPowers {{
 }};
 
 __device__ __forceinline__ void mass_upper(const TrigPowers& t, double* M) {{
-    const double* K = coef_table();
+    cdouble* const K = coef_table();
     [[maybe_unused]] const double c1 = t.c1, c2 = t.c2, c3 = t.c3, s1 = t.s1, s2 = t.s2, s3 = t.s3;
     [[maybe_unused]] const double {unpack};
 {chr(10).join(mlines)}
@@ -237,7 +240,7 @@ __device__ __forceinline__ void mass_upper(const TrigPowers& t, double* M) {{
 // dM/dq_J (J = 1..3), upper triangle
 template <int J>
 __device__ __forceinline__ void dmass_upper(const TrigPowers& t, double* dM) {{
-    const double* K = coef_table();
+    cdouble* const K = coef_table();
     [[maybe_unused]] const double c1 = t.c1, c2 = t.c2, c3 = t.c3, s1 = t.s1, s2 = t.s2, s3 = t.s3;
     [[maybe_unused]] const double {unpack};
 {chr(10).join(dlines)}
