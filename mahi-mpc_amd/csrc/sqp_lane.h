@@ -849,16 +849,27 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     double du[NU];
                     const gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
                     const gmem<FT>* const kk = (const gmem<FT>*)(kb + NU * 64) + lane;
+                    {
+                        // all loads of [K_k | kff_k] issued before the first use: under register pressure the
+                        // scheduler otherwise interleaves load -> vmcnt(0) -> fma, one memory round trip per gain
+                        FT kv[NU * NS];
+                        double kf[NU];
 #pragma unroll
-                    for (int a = 0; a < NU; ++a) {
-                        const int base = a * NS;
-                        double t = kb[a * 64 + lane];
+                        for (int a = 0; a < NU; ++a) kf[a] = kb[a * 64 + lane];
 #pragma unroll
-                        for (int q = 0; q < NX; ++q) t = fma((double)kk[(base + q) * 64], dx[q], t);
+                        for (int e = 0; e < NU * NS; ++e) kv[e] = kk[e * 64];
+                        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                        for (int c = 0; c < NU; ++c) t = fma((double)kk[(base + NX + c) * 64], dup[c], t);
-                        du[a] = t;
-                        SK(0, SF::DU, a) = t;
+                        for (int a = 0; a < NU; ++a) {
+                            const int base = a * NS;
+                            double t = kf[a];
+#pragma unroll
+                            for (int q = 0; q < NX; ++q) t = fma((double)kv[base + q], dx[q], t);
+#pragma unroll
+                            for (int c = 0; c < NU; ++c) t = fma((double)kv[base + NX + c], dup[c], t);
+                            du[a] = t;
+                            SK(0, SF::DU, a) = t;
+                        }
                     }
                     if (BOUNDED && pass + 1 < kBoundPasses) {  // a free control whose step crosses a bound: hold it
 #pragma unroll
