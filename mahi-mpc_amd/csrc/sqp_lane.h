@@ -173,7 +173,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     constexpr int NY = NX + NU;
     constexpr int SS = SF::SS;
     const int lane = threadIdx.x;
-    double* __restrict__ const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)lane_ws_doubles(NX, NU, NQ, N, XB) * 64);  // wave-uniform
+    double* const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)lane_ws_doubles(NX, NU, NQ, N, XB) * 64);  // wave-uniform
     const int kScratch = N + 1 + lane_lin_stages(NX, NU, NQ, XB);  // first stage of the W = P_xx A scratch
     constexpr bool WLDS = lane_w_in_lds(NX, NU, NQ);  // W's a-rows in the dead P~ slots, no HBM scratch
 #define ST(k, f, e) wsb[((int64_t)(k) * SS + (f) + (e)) * 64 + lane]  // one-off accesses
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                     double du[NU];
                     const gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
                     const gmem<FT>* const kk = (const gmem<FT>*)(kb + NU * 64) + lane;
-                    {
+                    if constexpr (!XB) {
                         // all loads of [K_k | kff_k] issued before the first use: under register pressure the
                         // scheduler otherwise interleaves load -> vmcnt(0) -> fma, one memory round trip per gain
                         FT kv[NU * NS];
@@ -867,6 +867,22 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
                             for (int q = 0; q < NX; ++q) t = fma((double)kv[base + q], dx[q], t);
 #pragma unroll
                             for (int c = 0; c < NU; ++c) t = fma((double)kv[base + NX + c], dup[c], t);
+                            du[a] = t;
+                            SK(0, SF::DU, a) = t;
+                        }
+                    } else {
+                        // interior-point variant: loads at their uses.  The batched-load form above, compiled for
+                        // the exo interior-point instantiation (256 VGPR + 256 AGPR + ~950 B/lane of spills), gave
+                        // lane-dependent wrong steps on gfx950 (non-converged instances in test_gpu_xbounds) although
+                        // it computes the same sums; this form is the one verified against the oracle.
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) {
+                            const int base = a * NS;
+                            double t = kb[a * 64 + lane];
+#pragma unroll
+                            for (int q = 0; q < NX; ++q) t = fma((double)kk[(base + q) * 64], dx[q], t);
+#pragma unroll
+                            for (int c = 0; c < NU; ++c) t = fma((double)kk[(base + NX + c) * 64], dup[c], t);
                             du[a] = t;
                             SK(0, SF::DU, a) = t;
                         }
