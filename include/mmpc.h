@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MMPC_ABI_VERSION 4
+#define MMPC_ABI_VERSION 5
 
 typedef struct mmpc_handle mmpc_handle;
 
@@ -198,6 +198,21 @@ int mmpc_solve_batch(mmpc_handle* h, int64_t B, const double* x0, const double* 
                      const double* traj, const double* weights, int64_t weights_stride,
                      const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
                      int32_t* iters, double* kkt_res, void* stream);
+
+/* mmpc_solve_batch that also writes u_0* [B][nu] -- the control calc_u returns, V[b][nx:nx+nu]
+ * (ModelControl.cpp:174-190) -- to u0_out (NULL = not written).  u0_out, status and iters may point into
+ * memory from mmpc_host_alloc: the kernel then stores the per-tick results straight into host memory and they
+ * are on the host when the stream's work completes (no copy kernel, no D2H; a controller loop reads them after
+ * synchronising the stream).  Since ABI 5. */
+int mmpc_solve_batch_u0(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev,
+                        const double* traj, const double* weights, int64_t weights_stride,
+                        const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
+                        int32_t* iters, double* kkt_res, double* u0_out, void* stream);
+
+/* Pinned host memory mapped into every device's address space at the same address (hipHostMalloc mapped |
+ * portable | coherent), for the outputs of mmpc_solve_batch_u0.  bytes = 0 gives *out = NULL.  Since ABI 5. */
+int mmpc_host_alloc(uint64_t bytes, void** out);
+int mmpc_host_free(void* p);
 
 /* Same contract with HOST pointers; synchronous (H2D, solve, D2H on an internal stream). */
 int mmpc_solve_batch_host(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev,

@@ -686,7 +686,8 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
 
 int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
                  const double* weights, int64_t w_stride, const double* u_lb, const double* u_ub, double* V,
-                 int32_t* status, int32_t* iters, double* kkt, hipStream_t stream, double* trace = nullptr) {
+                 int32_t* status, int32_t* iters, double* kkt, hipStream_t stream, double* trace = nullptr,
+                 double* u0_out = nullptr) {
     const mmpc_model_info& mi = h->info;
     if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
     if (B == 0) return MMPC_OK;
@@ -714,6 +715,7 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.iters = iters;
     p.kkt = kkt;
     p.trace = trace;
+    p.u0_out = u0_out;
     p.init_hold = h->opts.init_states == MMPC_INIT_HOLD_X0;
     p.init_zero = h->opts.init_states == MMPC_INIT_ZERO;
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
@@ -948,6 +950,14 @@ int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes) {
 int mmpc_solve_batch(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
                      const double* weights, int64_t weights_stride, const double* u_lb, const double* u_ub,
                      double* V_inout, int32_t* status, int32_t* iters, double* kkt_res, void* stream) {
+    return mmpc_solve_batch_u0(h, B, x0, u_prev, traj, weights, weights_stride, u_lb, u_ub, V_inout, status, iters,
+                               kkt_res, nullptr, stream);
+}
+
+int mmpc_solve_batch_u0(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
+                        const double* weights, int64_t weights_stride, const double* u_lb, const double* u_ub,
+                        double* V_inout, int32_t* status, int32_t* iters, double* kkt_res, double* u0_out,
+                        void* stream) {
     if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
     if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
     if (B == 0) return MMPC_OK;
@@ -958,7 +968,25 @@ int mmpc_solve_batch(mmpc_handle* h, int64_t B, const double* x0, const double* 
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
     return launch_solve(h, B, x0, u_prev, traj, weights, weights_stride, u_lb, u_ub, V_inout, status, iters,
-                        kkt_res, reinterpret_cast<hipStream_t>(stream));
+                        kkt_res, reinterpret_cast<hipStream_t>(stream), nullptr, u0_out);
+}
+
+int mmpc_host_alloc(uint64_t bytes, void** out) {
+    if (!out) return fail(MMPC_ERR_INVALID_ARG, "null output pointer");
+    *out = nullptr;
+    if (bytes == 0) return MMPC_OK;
+    // pinned, mapped into every device's address space at the same address, coherent (uncached on the device
+    // side): a kernel's stores land in host memory, visible to the host once the stream's work has completed
+    if (hipHostMalloc(out, bytes, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) != hipSuccess) {
+        *out = nullptr;
+        return fail(MMPC_ERR_HIP, "hipHostMalloc failed");
+    }
+    return MMPC_OK;
+}
+
+int mmpc_host_free(void* p) {
+    if (p && hipHostFree(p) != hipSuccess) return fail(MMPC_ERR_HIP, "hipHostFree failed");
+    return MMPC_OK;
 }
 
 int mmpc_solve_batch_host(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,

@@ -1431,6 +1431,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             for (int c = 0; c < NU; ++c) Vout[k * ND + NX + c] = sU[k * NU + c];
         }
     }
+    if (p.u0_out && gl < NU) p.u0_out[inst * NU + gl] = sU[gl];
     if (gl == 0) {
         if (p.status) p.status[inst] = status;
         if (p.iters) p.iters[inst] = it;

@@ -1084,6 +1084,10 @@ __global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw
     }
 #pragma unroll
     for (int r = 0; r < NX; ++r) Vout[N * ND + r] = ST(N, SF::X, r);
+    if (p.u0_out) {
+#pragma unroll
+        for (int c = 0; c < NU; ++c) p.u0_out[inst * NU + c] = ST(0, SF::U, c);
+    }
     if (p.status) p.status[inst] = status;
     if (p.iters) p.iters[inst] = it;
     if (p.kkt) p.kkt[inst] = kkt;

@@ -55,6 +55,9 @@ struct SolveParams {
     int32_t* status;
     int32_t* iters;
     double* kkt;
+    // u_0* [B][nu] (the control ModelControl::calc_u returns, ModelControl.cpp:174-190) or nullptr; may be
+    // host-mapped pinned memory (mmpc_host_alloc): the result then reaches the host without a copy
+    double* u0_out;
     double* trace;  // debug: [B][max_iter+1][8] per-iteration diagnostics, or nullptr
     int init_hold;  // mmpc_opts.init_states == MMPC_INIT_HOLD_X0: x_1..x_N start at x_0 (controls as given)
     int init_zero;  // mmpc_opts.init_states == MMPC_INIT_ZERO: V is not read, the iterate starts at 0 (x_0 pinned)
@@ -940,6 +943,7 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
         else v = sX[N * NX + r];
         Vout[i] = v;
     }
+    if (p.u0_out && lane < NU) p.u0_out[inst * NU + lane] = sU[lane];
     if (lane == 0) {
         if (p.status) p.status[inst] = status;
         if (p.iters) p.iters[inst] = it;

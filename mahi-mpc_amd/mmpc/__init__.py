@@ -104,6 +104,9 @@ def lib(path: str | None = None):
         L.mmpc_reserve_workspace.argtypes = [_vp, C.c_int64, C.POINTER(C.c_uint64)]
         L.mmpc_solve_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 7
         L.mmpc_solve_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 6
+        L.mmpc_solve_batch_u0.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 8
+        L.mmpc_host_alloc.argtypes = [C.c_uint64, C.POINTER(_vp)]
+        L.mmpc_host_free.argtypes = [_vp]
         L.mmpc_linearize_batch.argtypes = [_vp, C.c_int64] + [_vp] * 6
         L.mmpc_linearize_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 5
         L.mmpc_nlp_eval_batch.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 3
@@ -193,6 +196,39 @@ def _ptr(a):
     raise TypeError(type(a))
 
 
+class HostBuffer:
+    """Pinned host memory mapped into the devices' address space (mmpc_host_alloc): a solve kernel stores its
+    per-tick results (u_0*, status, iters) straight into it -- on the host once the stream has completed.
+    ``view(offset, dtype, count)`` gives numpy views; pass them (or their addresses) as solve outputs."""
+
+    def __init__(self, nbytes: int, path: str | None = None):
+        self._L = lib(path)
+        p = _vp()
+        rc = self._L.mmpc_host_alloc(int(nbytes), C.byref(p))
+        if rc != 0:
+            raise MmpcError(rc, self._L.mmpc_last_error().decode())
+        self.ptr = p.value or 0
+        self.nbytes = int(nbytes)
+        self._buf = (C.c_char * self.nbytes).from_address(self.ptr) if self.nbytes else None
+
+    def view(self, offset: int, dtype, count: int) -> np.ndarray:
+        dt = np.dtype(dtype)
+        assert offset % dt.itemsize == 0 and offset + count * dt.itemsize <= self.nbytes
+        return np.frombuffer(self._buf, dtype=dt, count=count, offset=offset)
+
+    def close(self):
+        if self.ptr:
+            self._buf = None
+            self._L.mmpc_host_free(self.ptr)
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def _f64(a, shape=None):
     a = np.ascontiguousarray(a, dtype=np.float64)
     if shape is not None:
@@ -259,10 +295,17 @@ class Solver:
 
     # ---- device-pointer API (torch tensors on the GPU or raw addresses) ----
     def solve_batch(self, B, x0, u_prev, traj, weights, V, status=None, iters=None, kkt=None,
-                    weights_stride=0, u_lb=None, u_ub=None, stream=None):
-        self._check(self._L.mmpc_solve_batch(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights),
-                                      weights_stride, _ptr(u_lb), _ptr(u_ub), _ptr(V), _ptr(status),
-                                      _ptr(iters), _ptr(kkt), stream))
+                    weights_stride=0, u_lb=None, u_ub=None, stream=None, u0=None):
+        """Device-pointer solve (stream-ordered).  u0: optional [B][nu] output of u_0* (mmpc_solve_batch_u0);
+        u0 / status / iters may be HostBuffer views (results stored by the kernel straight into host memory)."""
+        if u0 is None:
+            self._check(self._L.mmpc_solve_batch(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights),
+                                                 weights_stride, _ptr(u_lb), _ptr(u_ub), _ptr(V), _ptr(status),
+                                                 _ptr(iters), _ptr(kkt), stream))
+        else:
+            self._check(self._L.mmpc_solve_batch_u0(self._h, B, _ptr(x0), _ptr(u_prev), _ptr(traj), _ptr(weights),
+                                                    weights_stride, _ptr(u_lb), _ptr(u_ub), _ptr(V), _ptr(status),
+                                                    _ptr(iters), _ptr(kkt), _ptr(u0), stream))
 
     def synth(self, seed, first_index, B, x0, u_prev, traj, stream=None):
         self._check(self._L.mmpc_synth_batch(self._h, seed, first_index, B, _ptr(x0), _ptr(u_prev), _ptr(traj), stream))
