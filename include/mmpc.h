@@ -134,7 +134,7 @@ enum mmpc_hessian {
 };
 
 typedef struct mmpc_opts {
-    int32_t max_iter;   /* SQP iteration cap (reference IPOPT: 200, ModelControl.cpp:55). default 50 */
+    int32_t max_iter;   /* SQP iteration cap. default 200 (the reference IPOPT option, ModelControl.cpp:55) */
     int32_t device;     /* HIP device ordinal; -1 = the calling thread's current device. default -1 */
     double tol_grad;    /* ||grad_u J_reduced||_inf stop tolerance. default 1e-8 */
     double tol_defect;  /* ||g||_inf stop tolerance. default 1e-10 */

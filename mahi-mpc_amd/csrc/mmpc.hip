@@ -834,7 +834,7 @@ int mmpc_abi_version(void) { return MMPC_ABI_VERSION; }
 
 void mmpc_default_opts(mmpc_opts* o) {
     if (!o) return;
-    o->max_iter = 50;
+    o->max_iter = 200;  // reference IPOPT option, ModelControl.cpp:55
     o->device = -1;
     o->tol_grad = 1e-8;
     o->tol_defect = 1e-10;

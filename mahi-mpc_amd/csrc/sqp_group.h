@@ -1039,10 +1039,13 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         for (int a = 0; a < NU; ++a) Ku[a][c] = o[a];
                     }
                 }
-                // [K_k | kff_k] = -[K~ | kff~] (lane j < NS stores column j, lane NS the feed-forward column)
-                if (r <= NS) {
+                // [K_k | kff_k] = -[K~ | kff~] (lane j < NS stores column j, lanes >= NS the feed-forward column: kff
+                // is computed redundantly, bit-identical on every lane of the group, so the duplicate stores of the
+                // idle lanes write the same value -- no exec-mask branch in the sweep)
+                {
+                    const int col = r < NS ? r : NS;
 #pragma unroll
-                    for (int a = 0; a < NU; ++a) wK[(k * NU + a) * (NS + 1) + r] = -(r < NS ? Kcol[a] : kff[a]);
+                    for (int a = 0; a < NU; ++a) wK[(k * NU + a) * (NS + 1) + col] = -(r < NS ? Kcol[a] : kff[a]);
                 }
                 if constexpr (LAST) return;
                 // A^T P_xx A (row r) from the broadcast P_xx, p~_x = A^T mv + Q (x_k - r_{k-1})
@@ -1063,8 +1066,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     Ur[j] = colA(Prow[j], acol, pc);
                 }
                 at_mul<NQ, NA, double>(h, hFq, hFqd, Ur, Pn);
-                double pn = colA(mv, acol, mvb);
-                pn = lx ? fma(Qr, exr, pn) : (lu ? -Rr * duu : 0.0);
+                // x-lanes A^T mv + Q (x_k - r_{k-1}), u-lanes -R (u_k - u_{k-1}), idle lanes 0 -- blended with the
+                // lane-role factor (Rr = 0 off the u-lanes) instead of a branch
+                const double pn = fma(-Rr, duu, lxm * fma(Qr, exr, colA(mv, acol, mvb)));
                 // K~ columns of the other lanes
                 double Kb[NU][NX];
                 sfor<0, NX>([&](auto I) {
@@ -1265,10 +1269,22 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 };
                 Ops o0, o1;
                 fetch(0, o0);
-                if (N > 1) fetch(1, o1);
-                for (int k = 0; k < N; k += 2) {
-                    stage(k, o0);
-                    if (k + 1 < N) stage(k + 1, o1);
+                fetch(N > 1 ? 1 : 0, o1);
+                // both stages of the unrolled body unconditional (odd N: stage 0 peeled in front, the buffers swap
+                // roles): the loop top then has the same outstanding loads on every path, so the wait before stage
+                // k's operands is vmcnt(#loads of stage k+1), not vmcnt(0) -- a conditional second stage (or a
+                // tail stage) had the compiler drain the prefetch of k+2 at every stage pair
+                if (N & 1) {
+                    stage(0, o0);
+                    for (int k = 1; k < N; k += 2) {
+                        stage(k, o1);
+                        stage(k + 1, o0);
+                    }
+                } else {
+                    for (int k = 0; k < N; k += 2) {
+                        stage(k, o0);
+                        stage(k + 1, o1);
+                    }
                 }
             }
             __builtin_amdgcn_wave_barrier();

@@ -195,7 +195,7 @@ def synth(seed, first, B, N, h, model=TWO_LINK):
     return x0, up, tr
 
 
-def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=50,
+def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=200,
                 tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK, x_lb=None, x_ub=None,
                 init_states=0, hessian=HESS_GAUSS_NEWTON, solver=None):
     """solver: the GPU mmpc.Solver being checked -- the oracle then runs the Hessian that solver resolves for this

@@ -32,7 +32,7 @@ def test_library_is_gfx950_code_object(mmpc_mod):
 def test_abi_version_and_defaults(mmpc_mod):
     assert mmpc_mod.lib().mmpc_abi_version() == 5
     o = mmpc_mod.default_opts()
-    assert o.max_iter == 50 and o.device == -1
+    assert o.max_iter == 200 and o.device == -1   # ipopt.max_iter, ModelControl.cpp:55
     assert o.tol_grad == 1e-8 and o.tol_defect == 1e-10
     assert o.kkt_solver == mmpc_mod.KKT_AUTO
     assert o.hessian == mmpc_mod.HESSIAN_AUTO
