@@ -883,20 +883,29 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         auto backward_dist = [&](bool useW) {
             double Prow[NS], pvr;
             const double lxm = lx ? 1.0 : 0.0;
-            double nwr[KZ], nwu[NU * NU];   // W_k row rx and uu block, loaded one stage ahead from the workspace
-            auto load_w = [&](int k) {
-#pragma unroll
-                for (int j = 0; j < KZ; ++j) nwr[j] = lxm * wH[k * HW + rx * KZ + j];
-#pragma unroll
-                for (int j = 0; j < NU * NU; ++j) nwu[j] = wH[k * HW + NX * KZ + j];
+            // W_k row rx and uu block from the workspace, prefetched TWO stages ahead into alternating buffers
+            // (stage k reads buffer (N-1-k) & 1; one stage of distance left the load of W_{k-1}, an L2/MALL round
+            // trip, exposed at the top of every stage)
+            struct Wb {
+                double r[KZ], u[NU * NU];
             };
-            if (EXACT && useW) load_w(N - 1);
+            Wb w0, w1;
+            auto load_w = [&](int k, Wb& b) {
+#pragma unroll
+                for (int j = 0; j < KZ; ++j) b.r[j] = lxm * wH[k * HW + rx * KZ + j];
+#pragma unroll
+                for (int j = 0; j < NU * NU; ++j) b.u[j] = wH[k * HW + NX * KZ + j];
+            };
+            if (EXACT && useW) {
+                load_w(N - 1, w0);
+                load_w(N >= 2 ? N - 2 : 0, w1);
+            }
 #pragma unroll
             for (int j = 0; j < NS; ++j) Prow[j] = j < NX ? qoh[j] : 0.0;   // P~_N = blkdiag(Q, 0)
             pvr = Qr * (lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0);   // Q (x_N - r_{N-1})
             // (the sweep is issue-bound: its LDS operands are read in place; a prefetch buffer spills to AGPRs)
             // stage k; LAST = (k == 0), peeled so that the stages k >= 1 carry no k == 0 selects or branches
-            auto stage = [&](int k, auto last_c) {
+            auto stage = [&](int k, auto last_c, Wb& wb) {
                 constexpr bool LAST = decltype(last_c)::value;
                 double hFq[SQ], hFqd[FD], hFu[FU], cc[NX], u[NU], um[NU], acol[NA];
 #pragma unroll
@@ -922,10 +931,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 double wr[KZ], wu[NU * NU];
                 if constexpr (EXACT) {
 #pragma unroll
-                    for (int j = 0; j < KZ; ++j) wr[j] = useW ? nwr[j] : 0.0;
+                    for (int j = 0; j < KZ; ++j) wr[j] = useW ? wb.r[j] : 0.0;
 #pragma unroll
-                    for (int j = 0; j < NU * NU; ++j) wu[j] = useW ? nwu[j] : 0.0;
-                    if (!LAST && useW) load_w(k - 1);
+                    for (int j = 0; j < NU * NU; ++j) wu[j] = useW ? wb.u[j] : 0.0;
+                    if (!LAST && useW) load_w(k >= 2 ? k - 2 : 0, wb);   // k = 1: a harmless reload of stage 0
                 }
                 // T = P~ [B; I] (row r), mv = P~_x. c + p~ (row r)
                 double T[NU], mv = pvr;
@@ -1091,8 +1100,22 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 for (int a = 0; a < NU; ++a) pv2 = fma(-Ycol[a], kff[a], pv2);
                 pvr = pv2;
             };
-            for (int k = N - 1; k >= 1; --k) stage(k, std::false_type{});
-            stage(0, std::true_type{});
+            // inner stages N-1 .. 1 by unconditional pairs (an odd count peels stage N-1 in front), as the step sweep
+            using F_ = std::false_type;
+            if ((N - 1) & 1) {
+                stage(N - 1, F_{}, w0);
+                for (int k = N - 2; k >= 2; k -= 2) {
+                    stage(k, F_{}, w1);
+                    stage(k - 1, F_{}, w0);
+                }
+                stage(0, std::true_type{}, w1);
+            } else {
+                for (int k = N - 1; k >= 2; k -= 2) {
+                    stage(k, F_{}, w0);
+                    stage(k - 1, F_{}, w1);
+                }
+                stage(0, std::true_type{}, w0);
+            }
         };
         if constexpr (DIST) {
             d_recursion_dist();
