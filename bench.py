@@ -7,8 +7,10 @@ One "step" = one cold-started batched SQP solve of B independent instances per G
 nu=2, N=30, h=2 ms, fp64), i.e. what the reference does per control tick in ModelControl::calc_u
 (src/Mahi/Mpc/ModelControl.cpp:116-172) -- from V = 0 with x_0 pinned, the reference's first-call state -- for
 B instances at once, THROUGH RESULTS ON HOST: every step ends with the per-instance results the
-reference consumes (u_0*, status, iterations; ModelControl.cpp:160-190) copied into pinned host memory (N > 1:
-gathered to rank 0 over RCCL first, then copied to rank 0's host).  Inputs are generated on the device from
+reference consumes (u_0*, status, iterations; ModelControl.cpp:160-190) in pinned host memory -- stored there
+by the solve kernel itself (mmpc_solve_batch_u0 into mmpc_host_alloc memory, each rank into its own process's
+host memory); with N > 1 the last step's results of all ranks are also gathered to rank 0 (RCCL
+all_gather_into_tensor, then D2H) and checked there.  Inputs are generated on the device from
 (seed, global instance index) before the timed region (weak scaling: rank r solves global instances
 [r B, (r+1) B); results do not depend on the GPU count).
 
@@ -203,7 +205,9 @@ def run_rank(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     standin = args.standin
     if world > 1:
-        dist.init_process_group("gloo" if standin else "nccl")
+        # MMPC_BENCH_BACKEND / MMPC_BENCH_SAME_DEVICE: test hooks that rehearse the N > 1 GPU path on a one-GPU box
+        # (gloo ranks sharing device 0; RCCL rejects two ranks on one GPU) -- never set for measurements
+        dist.init_process_group(os.environ.get("MMPC_BENCH_BACKEND") or ("gloo" if standin else "nccl"))
     cfg = CONFIGS[args.config]
     B = args.batch or cfg["B"]
     N = args.horizon or cfg["N"]
@@ -220,6 +224,8 @@ def run_rank(args):
         stream = None
     else:
         import mmpc
+        if os.environ.get("MMPC_BENCH_SAME_DEVICE"):
+            local = 0
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
         tmpdir = tempfile.mkdtemp(prefix="mmpc_bench_")
@@ -245,12 +251,14 @@ def run_rank(args):
     V = torch.zeros((B, NV), **f64)
     # results the reference consumes per tick: u_0* (ModelControl.cpp:174-190), status, iterations -- one byte
     # buffer per rank, [B][nu] f64 u_0* | [B] i32 status | [B] i32 iterations.
-    # N = 1: the solve kernel stores them straight into pinned host memory (mmpc_solve_batch_u0 into an
-    #   mmpc_host_alloc buffer, two buffers alternating): no copy kernel, no D2H.
-    # N > 1: the solve writes status and iterations into a device buffer, u_0* is one strided copy out of V, one
-    #   all_gather_into_tensor (RCCL over xGMI) to rank 0's device, then one D2H there.
+    # Every step: the solve kernel stores them straight into pinned host memory of the rank's own process
+    #   (mmpc_solve_batch_u0 into an mmpc_host_alloc buffer, two buffers alternating): no copy kernel, no D2H --
+    #   each GPU process serves its own controllers (weak scaling).
+    # N > 1, last step (and last warm-up step): the rank-0 table instead -- the solve writes status and iterations
+    #   into a device buffer, u_0* is one strided copy out of V, one all_gather_into_tensor (RCCL over xGMI) to
+    #   rank 0's device, then one D2H there; rank 0 checks it against every rank's own results.
     nbytes = B * (8 * nu + 8)
-    zero_copy = world == 1 and not standin
+    zero_copy = not standin
     hbuf = None
     if zero_copy:
         hbuf = [mmpc.HostBuffer(nbytes) for _ in range(2)]
@@ -271,8 +279,11 @@ def run_rank(args):
     # MMPC_INIT_ZERO: the cold start V = 0 without reading V (no per-step memset); as_given zeroes V each step
     zero_v = args.init == "as_given" or standin
 
-    def results_to_host(k):
-        if zero_copy:
+    def zc(k, last):   # this step's results straight into host memory?
+        return zero_copy and (world == 1 or k != last)
+
+    def results_to_host(k, last):
+        if zc(k, last):
             return   # stored into host memory by the solve kernel
         u0.copy_(V[:, nx:nx + nu])
         if world > 1:   # N > 1: one all_gather_into_tensor (RCCL over xGMI) to rank 0's device, then D2H there
@@ -280,21 +291,21 @@ def run_rank(args):
         if rank == 0:
             host[k % 2].copy_(table, non_blocking=not standin)
 
-    def launch(k):
-        if zero_copy:
+    def launch(k, last):
+        if zc(k, last):
             u0h, sth, ith = hviews[k % 2]
             solver.solve_batch(B, x0, up, tr, w, V, sth, ith, None, stream=sh, u0=u0h)
         else:
             solver.solve_batch(B, x0, up, tr, w, V, st, it, None, stream=sh)
 
-    def solve(k):
+    def solve(k, last):
         if zero_v:
             V.zero_()   # cold start (reference first call: v_init = 0, ModelControl.cpp:29-50)
-        launch(k)
+        launch(k, last)
 
-    for k in range(args.warmup):
-        solve(k)
-        results_to_host(k)
+    for k in range(args.warmup):   # the last warm-up step also initialises the RCCL gather (N > 1)
+        solve(k, args.warmup - 1)
+        results_to_host(k, args.warmup - 1)
     sync = (lambda: torch.cuda.synchronize(dev)) if not standin else (lambda: None)
     sync()
     ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -308,11 +319,11 @@ def run_rank(args):
             if zero_v:
                 V.zero_()
             ev[k][0].record(stream)
-            launch(k)
+            launch(k, args.steps - 1)
             ev[k][1].record(stream)
         else:
-            solve(k)
-        results_to_host(k)
+            solve(k, args.steps - 1)
+        results_to_host(k, args.steps - 1)
     sync()
     if world > 1:
         dist.barrier()
@@ -320,14 +331,17 @@ def run_rank(args):
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else 0.0
     elapsed = mdist.max_over_ranks(elapsed, device=dev)
 
-    if zero_copy:   # the host buffer of the last step IS the result table; check it against V on the device
+    def hbytes(k):
+        return torch.from_numpy(np.frombuffer(hbuf[k % 2]._buf, dtype=np.uint8).copy())
+
+    zc_ok = True
+    if zero_copy and world == 1:   # the host buffer of the last step IS the result table; check it against V
         hb = hviews[(args.steps - 1) % 2]
-        res.copy_(torch.from_numpy(np.frombuffer(hbuf[(args.steps - 1) % 2]._buf, dtype=np.uint8).copy()))
+        res.copy_(hbytes(args.steps - 1))
         host[(args.steps - 1) % 2].copy_(res.cpu())
-        res_u0_dev = V[:, nx:nx + nu].cpu().numpy()
-        zc_ok = bool(np.array_equal(hb[0].reshape(B, nu), res_u0_dev))
-    else:
-        zc_ok = True
+        zc_ok = bool(np.array_equal(hb[0].reshape(B, nu), V[:, nx:nx + nu].cpu().numpy()))
+    elif zero_copy and args.steps >= 2:   # N > 1: the previous step (same instances) stored into host memory
+        zc_ok = bool(torch.equal(hbytes(args.steps - 2), res.cpu()))
     iters = it.cpu().numpy()
     status = st.cpu().numpy()
     # rank 0's host table of the last step against every rank's own results
@@ -335,7 +349,7 @@ def run_rank(args):
     ok = zc_ok
     if rank == 0:
         last = host[(args.steps - 1) % 2]
-        ok = bool(torch.equal(last[:nbytes], mine))
+        ok = bool(torch.equal(last[:nbytes], mine)) and zc_ok
         conv = sum(int((last[r * nbytes + B * nu * 8:r * nbytes + B * nu * 8 + 4 * B].view(torch.int32) == 0).sum())
                    for r in range(world))
         tail = last
@@ -369,11 +383,13 @@ def run_rank(args):
                    "init_states": {"zero": "reference cold start V = 0 (MMPC_INIT_ZERO: V not read)",
                                    "as_given": "reference cold start V = 0 (V zeroed every step)",
                                    "hold_x0": "x_1..x_N = x_0 (MMPC_INIT_HOLD_X0)"}[args.init],
-                   "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) gathered to "
-                                   "rank 0 by RCCL all_gather_into_tensor, then D2H into pinned memory"
+                   "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) stored by the "
+                                   "solve kernel into each rank's pinned host memory (mmpc_host_alloc); the last "
+                                   "step's table gathered to rank 0 by RCCL all_gather_into_tensor + D2H"
                                    if world > 1 else "batch-shard x1; per-step results (u_0*, status, iters) stored "
                                                      "by the solve kernel into pinned host memory (mmpc_host_alloc)"),
-                   "timed_region": "cold-start solve + results (u_0*, status, iters) on rank 0's host"},
+                   "timed_region": ("cold-start solves + per-step results (u_0*, status, iters) on the host"
+                                    + ("; the last step's table of all ranks on rank 0's host" if world > 1 else ""))},
         "converged": conv,
         "gathered_results_match": ok,
         "mean_sqp_iters": float(iters.mean()),
