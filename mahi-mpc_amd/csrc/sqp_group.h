@@ -1288,25 +1288,38 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     }
                     if (lu) sDU[k * NU + ru] = du;
                     sr = lx ? dxn : (lu ? du : 0.0);
-                    fetch(k + 2 < N ? k + 2 : N - 1, o);   // unconditional: static wait counts
+                    fetch(k + 3 < N ? k + 3 : N - 1, o);   // unconditional: static wait counts
                 };
-                Ops o0, o1;
+                // three buffers, refilled three stages ahead: the K rows come from L2/MALL (the workspace of a
+                // 512-instance XCD exceeds its 4 MB L2) and one stage of the sweep (~300 cycles) did not cover that
+                // latency -- with two buffers every stage waited for the loads issued one stage earlier
+                Ops o0, o1, o2;
                 fetch(0, o0);
                 fetch(N > 1 ? 1 : 0, o1);
-                // both stages of the unrolled body unconditional (odd N: stage 0 peeled in front, the buffers swap
-                // roles): the loop top then has the same outstanding loads on every path, so the wait before stage
-                // k's operands is vmcnt(#loads of stage k+1), not vmcnt(0) -- a conditional second stage (or a
-                // tail stage) had the compiler drain the prefetch of k+2 at every stage pair
-                if (N & 1) {
+                fetch(N > 2 ? 2 : 0, o2);
+                // all three stages of the unrolled body unconditional (N mod 3 stages peeled in front, the buffers
+                // rotate roles): the loop top then has the same outstanding loads on every path, so the wait before
+                // stage k's operands is vmcnt(#loads of stages k+1, k+2), not vmcnt(0)
+                if (N % 3 == 1) {
                     stage(0, o0);
-                    for (int k = 1; k < N; k += 2) {
+                    for (int k = 1; k < N; k += 3) {
                         stage(k, o1);
+                        stage(k + 1, o2);
+                        stage(k + 2, o0);
+                    }
+                } else if (N % 3 == 2) {
+                    stage(0, o0);
+                    stage(1, o1);
+                    for (int k = 2; k < N; k += 3) {
+                        stage(k, o2);
                         stage(k + 1, o0);
+                        stage(k + 2, o1);
                     }
                 } else {
-                    for (int k = 0; k < N; k += 2) {
+                    for (int k = 0; k < N; k += 3) {
                         stage(k, o0);
                         stage(k + 1, o1);
+                        stage(k + 2, o2);
                     }
                 }
             }
