@@ -152,7 +152,10 @@ __device__ __forceinline__ gmem<double>* stage_ptr(double* wsb, int64_t k, int S
 // merit and iterates stay fp64, so every SQP iteration refines the fp32 step against fp64 residuals).
 // XB: state bounds, the primal-dual interior-point variant (oracle solve_one_ip; see sqp_group.h)
 template <class Model, class FT = double, bool BOUNDED = false, bool XB = false>
-__global__ __launch_bounds__(64) void sqp_lane_kernel(SolveParams p, LaneWork lw) {
+// one wave per SIMD by design (P~ in LDS, ~40 KB per wave): telling the scheduler so lets it schedule for latency
+// rather than for a second wave's registers (cfg#3: 12.06 -> 11.94 ms)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_lane_kernel(SolveParams p,
+                                                                                                 LaneWork lw) {
     static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
     constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)

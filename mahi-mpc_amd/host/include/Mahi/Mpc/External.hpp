@@ -10,7 +10,10 @@
 #pragma once
 #include <memory>
 #include <string>
+#include <type_traits>
 #include <vector>
+
+#include <Mahi/Mpc/SX.hpp>
 
 namespace mahi {
 namespace mpc {
@@ -21,6 +24,15 @@ public:
     // evaluate with dense inputs (sizes nrow*ncol of each input sparsity); returns dense outputs.
     // Throws std::invalid_argument on a size mismatch and std::runtime_error if the function reports failure.
     std::vector<std::vector<double>> operator()(const std::vector<std::vector<double>>& args) const;
+    // the reference's call shape: std::vector<casadi::DM> in, std::vector<casadi::DM> out
+    // (examples/model_control_example.cpp:81-82)
+    // (a template, so that a braced list {state, control} still selects the overload above)
+    template <class D, class = typename std::enable_if<std::is_same<D, DM>::value>::type>
+    std::vector<DM> operator()(const std::vector<D>& args) const {
+        std::vector<std::vector<double>> in(args.begin(), args.end());
+        auto out = (*this)(in);
+        return std::vector<DM>(out.begin(), out.end());
+    }
     const std::string& name() const;
     long long n_in() const;
     long long n_out() const;
@@ -38,3 +50,7 @@ External external(const std::string& name, const std::string& library_path);
 
 }  // namespace mpc
 }  // namespace mahi
+
+namespace casadi {
+using mahi::mpc::external;
+}  // namespace casadi

@@ -10,7 +10,9 @@
 #include <thread>
 #include <vector>
 
+#include <Mahi/Mpc/External.hpp>
 #include <Mahi/Mpc/ModelParameters.hpp>
+#include <Mahi/Mpc/SX.hpp>
 #include <Mahi/Util/Time.hpp>
 
 struct mmpc_handle;
@@ -99,3 +101,7 @@ private:
 
 }  // namespace mpc
 }  // namespace mahi
+
+namespace casadi {
+using mahi::mpc::Dict;   // the solver_opts type of the reference's constructor (ModelControl.hpp:26)
+}  // namespace casadi

@@ -196,4 +196,12 @@ using mahi::mpc::Function;
 using mahi::mpc::inf;
 using mahi::mpc::SX;
 using mahi::mpc::SXDict;
+// casadi's stream operator for std::vector ("[a, b, c]"), which the reference's examples reach through
+// `using namespace casadi;` (model_control_example.cpp:104 writes `file << time_result`)
+template <class T>
+std::ostream& operator<<(std::ostream& os, const std::vector<T>& v) {
+    os << "[";
+    for (size_t i = 0; i < v.size(); ++i) os << (i ? ", " : "") << v[i];
+    return os << "]";
+}
 }  // namespace casadi
