@@ -204,6 +204,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     // lane-role masks as blend factors: the DIST loops blend loaded values with FMAs instead of selects (a select
     // of an LDS load becomes a branch or a pointer select)
     const double lqd = r < NQ ? 1.0 : 0.0, lad = la ? 1.0 : 0.0;
+    // x-lane factor for the sweeps' per-stage masking: one FP64 multiply where a 64-bit select is two cndmasks (the
+    // masked values are finite sums of this instance's own data, so 0 * v == 0)
+    const double lxf = lx ? 1.0 : 0.0;
     const int rq = r < NQ ? r : 0;                    // q column of a q-lane (clamped)
     const double Rr = lu ? w[NX + ru] : 0.0;          // R of this lane's u row
     double hq[NQ > 0 ? NQ : 1], hrow[NX], qoh[NX], rdg[NU];
@@ -729,7 +732,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         // column r of A (x-lanes): own row (identity) + h in row z for r = NQ + z + acol[t] in row NQ + t, where
         // acol = hFq[:, r] (q-lanes) or hFqd[:, r - NQ] (a-lanes); so (A^T v)[r] = colA(v_r, vb) with vb = all v.
         auto colA = [&](double own, const double* acol, const double* vb) {
-            double t = lx ? own : 0.0;
+            double t = lxf * own;
 #pragma unroll
             for (int z = 0; z < NQ; ++z) t = fma(hq[z], vb[z], t);
 #pragma unroll
@@ -779,7 +782,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     if (j & 1) t1 = fma(arow[j], db[j], t1);
                     else t0 = fma(arow[j], db[j], t0);
                 }
-                dr = lx ? t0 + t1 : 0.0;
+                dr = lxf * (t0 + t1);
                 if (lx) sD[(k + 1) * NX + rx] = dr;
             }
         };
@@ -850,7 +853,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 gmax = fmax(gmax, lum * fabs(2.0 * g));   // u-lanes only (0 elsewhere)
                 nonfinite |= lu && !isfinite(g);
                 if constexpr (!LAST) {   // (A^T lam)[r] + Q e_{k-1}[r], two partial sums
-                    double t0 = lx ? lamr + qe : 0.0, t1 = 0.0;
+                    double t0 = lxf * (lamr + qe), t1 = 0.0;
 #pragma unroll
                     for (int z = 0; z < NQ; ++z) t1 = fma(hq[z], lamb[z], t1);
 #pragma unroll
@@ -858,7 +861,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         if (s2 & 1) t1 = fma(acol[s2], lamb[NQ + s2], t1);
                         else t0 = fma(acol[s2], lamb[NQ + s2], t0);
                     }
-                    lamr = lx ? t0 + t1 : 0.0;
+                    lamr = lxf * (t0 + t1);
                     lmax = fmax(lmax, fabs(lamr));
                     if (EXACT && lx) sD[k * NX + rx] = lamr;
                 }

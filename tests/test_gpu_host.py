@@ -138,3 +138,20 @@ def test_calc_u_batch_enforces_control_limits(oracle, tmp_path):
     assert (np.abs(U) == lim).any()   # the limits bind for some of these instances
     o = oracle.solve_batch(N, 0.002, x0, up, tr, np.array(WEIGHTS_CFG), u_lb=[-lim, -lim], u_ub=[lim, lim])
     np.testing.assert_allclose(V, o["V"], rtol=0, atol=1e-9 * np.abs(o["V"]).max())
+
+
+def test_threaded_loop_example(model_json, tmp_path):
+    """ModelControl's worker thread (start_calc / set_state / control_at_time / stop_calc, ModelControl.cpp:75-114)
+    in the reference's threaded example loop (thread_model_control_example.cpp:53-120, with Rm given): a 1 kHz
+    plant thread publishes snapshots while the worker solves from the latest one on the GPU; every applied control
+    is finite, the last solve converged, and the arm follows the 1 rad sinusoid (tracking error below its
+    amplitude in the second half).  The TSan build of the same loop: tools/tsan_build.sh + tools/tsan_run.sh."""
+    subprocess.run(["make", "-s", "-C", HOST], check=True)
+    exe = os.path.join(HOST, "bin", "model_control_example")
+    out = subprocess.run([exe, "20", "0.5", "n", "-", "thread"], cwd=tmp_path, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    line = [l for l in out.stdout.splitlines() if l.startswith("thread,")][-1].split(",")
+    ticks, status, umax, err, finite = int(line[1]), int(line[2]), float(line[3]), float(line[4]), int(line[5])
+    assert ticks >= 400 and finite == 1 and status == 0, line
+    assert 0 < umax < 1e3 and err < 1.0, line
