@@ -231,7 +231,7 @@ def test_bounds_enforced(model_json, mmpc_mod, oracle):
     assert (r["status"] == 0).all()
     r = s.solve_batch_host(x0, up, tr, w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
     o = oracle.solve_batch(30, H, x0, up, tr, w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
-    _compare(r, o, tol_same=1e-8)
+    _compare(r, o)
     assert (r["status"] == 0).all()
     assert np.abs(r["V"][:, [6 * k + 4 + c for k in range(30) for c in range(2)]]).max() <= 1e-3
 

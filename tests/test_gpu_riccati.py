@@ -178,7 +178,7 @@ def test_exo_cfg5_full_batch_properties(exo_solver, oracle, torch_cuda):
     gpu, o, J = _exo_full_batch(exo_solver, oracle, torch_cuda, 1)
     assert (o["status"] == 0).all()
     assert _rel(gpu["V"], o["V"]).max() <= 1e-6
-    np.testing.assert_allclose(J, o["J"], rtol=1e-9)
+    np.testing.assert_allclose(J, o["J"], rtol=1e-10)
 
 
 def test_riccati_two_link_matches_condensed_and_oracle(model_json, mmpc_mod, oracle, torch_cuda):
