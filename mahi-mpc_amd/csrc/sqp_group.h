@@ -796,9 +796,11 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 acol[t2] = v;
             }
         };
-        // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1} (lam_N = Q e_{N-1}, e_{k-1} = d_k + x_k - r_{k-1}) and the
-        // reduced gradient g_k = B_k^T lam_{k+1} + R (u_k - u_{k-1}) + Rm u_k - R (u_{k+1} - u_k): lane r holds
-        // lam[r] (x-lanes) and g_k[r - NX] (u-lanes); gmax, lmax are per-lane maxima (reduced by the caller).
+        // adjoint lam_k = Q e_{k-1} + A_k^T lam_{k+1} (lam_N = Q e_{N-1}, e_{k-1} = d_k + x_k - r_{k-1}), lane r holds
+        // lam[r] (x-lanes) and writes it over d_k in sD (d_k is read one stage earlier); then, stage-parallel, the
+        // reduced gradient g_k = B_k^T lam_{k+1} + R (u_k - u_{k-1}) + Rm u_k - R (u_{k+1} - u_k) from the stored
+        // lam (the serial sweep carries only the lam chain: the gradient's loads and arithmetic were a quarter of
+        // its instructions).  gmax, lmax are per-lane maxima (reduced by the caller).
         // Runs before the stop test, so a converged wave skips the Riccati sweep.
         auto adjoint_dist = [&]() {
             double lamr;
@@ -806,82 +808,59 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 const double eb = lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0;   // x_N - r_{N-1}
                 lamr = Qr * (sD[N * NX + rx] + eb);
                 lmax = fmax(lmax, fabs(lamr));
-                if (EXACT && lx) sD[N * NX + rx] = lamr;   // lam_k replaces d_k (read one stage earlier)
+                if (lx) sD[N * NX + rx] = lamr;   // lam_k replaces d_k (read one stage earlier)
             }
-            const double Rmr = lu ? w[NX + NU + ru] : 0.0;   // Rm of this lane's u row
-            const double upr = p.u_prev[ii * NU + ru];
-            const double lum = lu ? 1.0 : 0.0;
-            double unx = 0.0;                                  // u_{k+1}[ru]
-            // stage operands (loaded one stage ahead): column r of A's a-rows, column ru of hFu, u_k[ru],
-            // u_{k-1}[ru], Q (d_k + x_k - r_{k-1})[r]
-            double nacol[NA], nhfu[NA], nuk, num, nqe = 0.0;
-            auto load = [&](int k, auto zero_c) {   // zero_c: k == 0 (u_{-1} = u_prev, no Q e_{-1})
-                constexpr bool ZERO = decltype(zero_c)::value;
+            // stage operands (loaded one stage ahead): column r of A's a-rows, Q (d_k + x_k - r_{k-1})[r]
+            double nacol[NA], nqe = 0.0;
+            auto load = [&](int k) {   // k >= 1
                 load_acol(k, nacol);
-#pragma unroll
-                for (int s2 = 0; s2 < NA; ++s2) nhfu[s2] = sFu[k * FU + s2 * NU + ru];
-                nuk = sU[k * NU + ru];
-                if constexpr (ZERO) {
-                    num = upr;
-                } else {
-                    num = sU[(k - 1) * NU + ru];
-                    const double xk = sX[k * NX + rx], trm = tr[(k - 1) * NX + rx], dk = sD[k * NX + rx];
-                    nqe = Qr * (dk + (xk - trm));
-                }
+                const double xk = sX[k * NX + rx], trm = tr[(k - 1) * NX + rx], dk = sD[k * NX + rx];
+                nqe = Qr * (dk + (xk - trm));
             };
-            // stage k: FIRST = (k == N - 1, no u_{k+1}), LAST = (k == 0, no lam_k); peeled so that the inner
-            // stages carry no k-dependent selects or branches
-            auto stage = [&](int k, auto first_c, auto last_c, auto next0_c) {   // NEXT0: k == 1
-                constexpr bool FIRST = decltype(first_c)::value, LAST = decltype(last_c)::value;
-                constexpr bool NEXT0 = decltype(next0_c)::value;
-                double acol[NA], hfu[NA];
+            // stage k >= 1: lam_k from lam_{k+1}; PREFETCH: load stage k - 1's operands (k >= 2)
+            auto stage = [&](int k, auto prefetch_c) {
+                constexpr bool PREFETCH = decltype(prefetch_c)::value;
+                double acol[NA];
 #pragma unroll
-                for (int s2 = 0; s2 < NA; ++s2) {
-                    acol[s2] = nacol[s2];
-                    hfu[s2] = nhfu[s2];
-                }
-                const double uk = nuk, um = num, qe = nqe;
-                if constexpr (!LAST) load(k - 1, std::integral_constant<bool, NEXT0>{});
+                for (int s2 = 0; s2 < NA; ++s2) acol[s2] = nacol[s2];
+                const double qe = nqe;
+                if constexpr (PREFETCH) load(k - 1);
                 double lamb[NX];
                 sfor<0, NX>([&](auto I) { lamb[I] = row_bcast<I>(lamr); });
-                double g = 0.0;
+                // (A^T lam)[r] + Q e_{k-1}[r], two partial sums
+                double t0 = lxf * (lamr + qe), t1 = 0.0;
 #pragma unroll
-                for (int s2 = 0; s2 < NA; ++s2) g = fma(hfu[s2], lamb[NQ + s2], g);
-                g = fma(Rr, uk - um, fma(Rmr, uk, g));
-                if constexpr (!FIRST) g -= Rr * (unx - uk);
-                unx = uk;
-                gmax = fmax(gmax, lum * fabs(2.0 * g));   // u-lanes only (0 elsewhere)
-                nonfinite |= lu && !isfinite(g);
-                if constexpr (!LAST) {   // (A^T lam)[r] + Q e_{k-1}[r], two partial sums
-                    double t0 = lxf * (lamr + qe), t1 = 0.0;
+                for (int z = 0; z < NQ; ++z) t1 = fma(hq[z], lamb[z], t1);
 #pragma unroll
-                    for (int z = 0; z < NQ; ++z) t1 = fma(hq[z], lamb[z], t1);
-#pragma unroll
-                    for (int s2 = 0; s2 < NA; ++s2) {
-                        if (s2 & 1) t1 = fma(acol[s2], lamb[NQ + s2], t1);
-                        else t0 = fma(acol[s2], lamb[NQ + s2], t0);
-                    }
-                    lamr = lxf * (t0 + t1);
-                    lmax = fmax(lmax, fabs(lamr));
-                    if (EXACT && lx) sD[k * NX + rx] = lamr;
+                for (int s2 = 0; s2 < NA; ++s2) {
+                    if (s2 & 1) t1 = fma(acol[s2], lamb[NQ + s2], t1);
+                    else t0 = fma(acol[s2], lamb[NQ + s2], t0);
                 }
+                lamr = lxf * (t0 + t1);
+                lmax = fmax(lmax, fabs(lamr));
+                if (lx) sD[k * NX + rx] = lamr;
             };
-            using T_ = std::true_type;
-            using F_ = std::false_type;
-            if (N == 1) {
-                load(0, T_{});
-                stage(0, T_{}, T_{}, F_{});
-                return;
+            if (N >= 2) {
+                load(N - 1);
+                for (int k = N - 1; k >= 2; --k) stage(k, std::true_type{});
+                stage(1, std::false_type{});
             }
-            load(N - 1, F_{});
-            if (N == 2) {
-                stage(1, T_{}, F_{}, T_{});
-            } else {
-                stage(N - 1, T_{}, F_{}, F_{});
-                for (int k = N - 2; k >= 2; --k) stage(k, F_{}, F_{}, F_{});
-                stage(1, F_{}, F_{}, T_{});
+            // the lam rows of the other lanes of this wave must be visible to the gradient pass
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            for (int k = gl; k < N; k += G) {
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {
+                    double g = 0.0;
+#pragma unroll
+                    for (int s2 = 0; s2 < NA; ++s2) g = fma(sFu[k * FU + s2 * NU + c], sD[(k + 1) * NX + NQ + s2], g);
+                    const double uk = sU[k * NU + c], um = k == 0 ? up[c] : sU[(k - 1) * NU + c];
+                    g = fma(R[c], uk - um, fma(Rm[c], uk, g));
+                    if (k < N - 1) g -= R[c] * (sU[(k + 1) * NU + c] - uk);
+                    gmax = fmax(gmax, fabs(2.0 * g));
+                    nonfinite |= !isfinite(g);
+                }
             }
-            stage(0, F_{}, T_{}, F_{});
         };
         auto backward_dist = [&](bool useW) {
             double Prow[NS], pvr;
