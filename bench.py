@@ -510,6 +510,8 @@ def roofline(args, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms):
             "pmc_fp64_valu_frac_issued": (pmc["fp64_valu_flops_issued_per_launch"] / sec / 1e12 / FP64_PEAK_TFLOPS
                                           if pmc.get("fp64_valu_flops_issued_per_launch") else None),
             "pmc_mfma_counters": pmc.get("mfma_counters"),
+            "pmc_lds_bank_conflict_cycles_per_launch": pmc.get("lds_bank_conflict_cycles"),
+            "pmc_valu_active_frac": pmc.get("valu_active_frac"),
             "note": "frac = the kernel's own algorithmic flops / FP64 vector peak (no kernel issues MFMA: DESIGN.md "
                     "'Why no MFMA'); pmc_* = rocprofv3 counters of the same kernel (tools/pmc.sh) when they match "
                     "this run's shape and kernel time: issued FP64 VALU lane-flops incl. inactive-lane slots"}

@@ -71,5 +71,9 @@ if a.traffic_json and a.key and "hbm_bytes_per_launch" in res:
                  "hbm_bytes_per_launch": res["hbm_bytes_per_launch"],
                  "kernel_ms_at_measurement": res.get("kernel_ms_trace_pass"),
                  "fp64_valu_flops_issued_per_launch": res.get("fp64_valu_flops_issued_per_launch"),
-                 "mfma_counters": res["mfma_counters"], "source": a.source}
+                 "mfma_counters": res["mfma_counters"],
+                 "lds_bank_conflict_cycles": summary.get("SQ_LDS_BANK_CONFLICT"),
+                 "valu_active_frac": (summary["SQ_ACTIVE_INST_VALU"] / summary["SQ_WAVE_CYCLES"]
+                                      if summary.get("SQ_WAVE_CYCLES") and "SQ_ACTIVE_INST_VALU" in summary else None),
+                 "source": a.source}
     json.dump(tj, open(a.traffic_json, "w"), indent=1)
