@@ -78,8 +78,12 @@ def parse(argv=None):
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--tol", type=float, default=None,
                     help="outer tolerance: tol_grad = tol, tol_defect = tol/100 (default: 1e-8 / 1e-10)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline wall time")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0,
+                    help="target wall time of each CPU-baseline leg (Riccati, dense condensed)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="cfg2 only: skip the cfg#3 / cfg#5 lines the default invocation attaches as 'secondary'")
+    ap.add_argument("--no-sweep", action="store_true", help="cfg5: skip the tolerance sweep (single tolerance)")
     ap.add_argument("--init", choices=["zero", "as_given", "hold_x0"], default="zero",
                     help="mmpc_opts.init_states: the reference's cold start V = 0 (zero: MMPC_INIT_ZERO, V not read; "
                          "as_given: V zeroed every step), or x_1..x_N = x_0 (DESIGN 3d)")
@@ -130,43 +134,70 @@ def launch(args, argv) -> int:
 
 
 # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1 only)
-def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1):
-    """Oracle (oracle/liboracle.so: the same NLP and SQP in plain C + OpenMP, dense condensed KKT) on a
-    bounded sample of the same seeded workload, plus its agreement with the GPU on the shared instances."""
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle_lib as o
-    model = o.EXO if cfg["model"] == "exo_arm" else o.TWO_LINK
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+def _cpu_leg(o, cfg, N, h, target_s, kw, kkt):
+    """one timed oracle leg on a bounded sample: a small calibration solve sizes the sample to ~target_s"""
+    model = kw["model"]
     w = np.array(cfg["weights"])
-    # the same SQP as the GPU: the Hessian the library resolved (mmpc_resolve_hessian: 1 Gauss-Newton, 2 exact)
-    kw = dict(nthreads=threads, model=model, tol_grad=tol_grad, tol_defect=tol_defect,
-              hessian=o.HESS_EXACT if hessian == 2 else o.HESS_GAUSS_NEWTON)
-    n0 = 2 * threads
+    n0 = 2 * kw["nthreads"]
     x0, up, tr = o.synth(SEED, 0, n0, N, h, model=model)
     t = time.perf_counter()
-    o.solve_batch(N, h, x0, up, tr, w, **kw)
+    o.solve_batch(N, h, x0, up, tr, w, kkt=kkt, **kw)
     dt = time.perf_counter() - t
     n = int(max(n0, min(200000, n0 * target_s / max(dt, 1e-6))))
     x0, up, tr = o.synth(SEED, 0, n, N, h, model=model)
     t = time.perf_counter()
-    r = o.solve_batch(N, h, x0, up, tr, w, **kw)
-    dt = time.perf_counter() - t
-    m = min(n, gpu_V.shape[0])
-    ref = r["V"][:m]
-    scale = np.maximum(np.abs(ref).max(axis=1), 1e-300)
-    rel = np.abs(gpu_V[:m] - ref).max(axis=1) / scale
-    same_it = r["iters"][:m] == gpu_iters[:m]
+    r = o.solve_batch(N, h, x0, up, tr, w, kkt=kkt, **kw)
+    return n, time.perf_counter() - t, r
+
+
+def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1):
+    """The oracle (oracle/liboracle.so: the same NLP and SQP in plain C + OpenMP, cold start V = 0) timed on a
+    bounded sample of the same seeded workload, in two legs:
+      riccati          the Riccati recursion the GPU kernels run (ORACLE_KKT_RICCATI: same algorithm, same iterates)
+                       -- the reported value;
+      dense_condensed  explicit condensing + dense Cholesky of the N*nu Hessian (the oracle's default checker).
+    Each leg's agreement with the GPU on the shared instances is reported beside it."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as o
+    model = o.EXO if cfg["model"] == "exo_arm" else o.TWO_LINK
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    # the same SQP as the GPU: the Hessian the library resolved (mmpc_resolve_hessian: 1 Gauss-Newton, 2 exact)
+    kw = dict(nthreads=threads, model=model, tol_grad=tol_grad, tol_defect=tol_defect, init_states=2,
+              hessian=o.HESS_EXACT if hessian == 2 else o.HESS_GAUSS_NEWTON)
     hist = lambda a: {int(k): int(v) for k, v in zip(*np.unique(a, return_counts=True))}  # noqa: E731
-    return dict(value=n / dt, unit="solves/s", cores=threads, kind="port",
-                sample=f"first {n} {cfg['workload'].split(':')[0]} instances (seed {SEED}), cold start, {dt:.1f} s "
-                       f"wall, {int((r['status'] == 0).sum())}/{n} converged; oracle SQP with a DENSE condensed "
-                       f"KKT (Cholesky of the N*nu Hessian, not the Riccati recursion the GPU runs), "
-                       f"{'exact' if hessian == 2 else 'Gauss-Newton'} Hessian as the GPU, "
-                       f"{threads} OpenMP threads",
-                vs_gpu=dict(instances=int(m), max_rel_diff_V=float(rel.max()),
-                            max_rel_diff_V_same_iters=float(rel[same_it].max()) if same_it.any() else None,
-                            same_iteration_count=int(same_it.sum())),
-                iters_hist_cpu=hist(r["iters"]), iters_hist_gpu=hist(gpu_iters))
+    legs = {}
+    for name, kkt, what in (("riccati", o.KKT_RICCATI, "Riccati recursion on [dx_k; du_{k-1}] (the GPU's algorithm)"),
+                            ("dense_condensed", o.KKT_DENSE, "DENSE condensed KKT (Cholesky of the N*nu Hessian)")):
+        n, dt, r = _cpu_leg(o, cfg, N, h, target_s, kw, kkt)
+        m = min(n, gpu_V.shape[0])
+        ref = r["V"][:m]
+        scale = np.maximum(np.abs(ref).max(axis=1), 1e-300)
+        rel = np.abs(gpu_V[:m] - ref).max(axis=1) / scale
+        same_it = r["iters"][:m] == gpu_iters[:m]
+        legs[name] = dict(
+            value=n / dt, unit="solves/s", cores=threads,
+            sample=f"first {n} {cfg['workload'].split(':')[0]} instances (seed {SEED}), cold start, {dt:.1f} s wall, "
+                   f"{int((r['status'] == 0).sum())}/{n} converged; oracle SQP with a {what}, "
+                   f"{'exact' if hessian == 2 else 'Gauss-Newton'} Hessian as the GPU, {threads} OpenMP threads",
+            vs_gpu=dict(instances=int(m), max_rel_diff_V=float(rel.max()),
+                        max_rel_diff_V_same_iters=float(rel[same_it].max()) if same_it.any() else None,
+                        same_iteration_count=int(same_it.sum())),
+            iters_hist_cpu=hist(r["iters"]))
+    ric = legs["riccati"]
+    return dict(value=ric["value"], unit="solves/s", cores=threads, kind="port",
+                sample=ric["sample"] + " (the dense-condensed leg is reported beside it)",
+                vs_gpu=ric["vs_gpu"], iters_hist_cpu=ric["iters_hist_cpu"], iters_hist_gpu=hist(gpu_iters),
+                riccati=ric, dense_condensed=legs["dense_condensed"])
+
+
+def lib_sha256(path: str) -> str:
+    """sha256 of the solver library a run loaded: the key that ties a PMC summary to the build it measured"""
+    import hashlib
+    hsh = hashlib.sha256()
+    with open(path, "rb") as fh:
+        for chunk in iter(lambda: fh.read(1 << 20), b""):
+            hsh.update(chunk)
+    return hsh.hexdigest()
 
 
 # ------------------------------------------------------------------ test stand-in (no GPU)
@@ -198,19 +229,36 @@ class _StandInSolver:
 def run_rank(args):
     import torch
     import torch.distributed as dist
-    import mmpc.dist as mdist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    standin = args.standin
     if world > 1:
         # MMPC_BENCH_BACKEND / MMPC_BENCH_SAME_DEVICE: test hooks that rehearse the N > 1 GPU path on a one-GPU box
         # (gloo ranks sharing device 0; RCCL rejects two ranks on one GPU) -- never set for measurements
-        dist.init_process_group(os.environ.get("MMPC_BENCH_BACKEND") or ("gloo" if standin else "nccl"))
-    cfg = CONFIGS[args.config]
-    B = args.batch or cfg["B"]
-    N = args.horizon or cfg["N"]
+        dist.init_process_group(os.environ.get("MMPC_BENCH_BACKEND") or ("gloo" if args.standin else "nccl"))
+    out = run_config(args, args.config, world, rank, primary=True)
+    # the default (headline) invocation also measures the exo workloads of SURVEY.md 8d inside the same run, so the
+    # driver's clock covers them: cfg#3 (at N > 1 ranks: cfg#4, weak-scaled 65536 instances per GPU) and cfg#5
+    if args.config == "cfg2" and not args.no_secondary and not args.standin and args.batch is None \
+            and args.horizon is None:
+        out["secondary"] = {c: run_config(args, c, world, rank, primary=False) for c in ("cfg3", "cfg5")}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_config(args, name, world, rank, primary=True):
+    """W warm-up + K timed steps of config `name` on this rank; returns the JSON object of the line (rank 0)."""
+    import torch
+    import torch.distributed as dist
+    import mmpc.dist as mdist
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    standin = args.standin
+    cfg = CONFIGS[name]
+    B = (args.batch if primary else None) or cfg["B"]
+    N = (args.horizon if primary else None) or cfg["N"]
     nx, nu, h_us = cfg["nx"], cfg["nu"], 2000
     h = h_us * 1e-6
     tol_grad = 1e-8 if args.tol is None else args.tol
@@ -231,13 +279,13 @@ def run_rank(args):
         tmpdir = tempfile.mkdtemp(prefix="mmpc_bench_")
         path = mmpc.write_model_json(os.path.join(tmpdir, f"{cfg['model']}.json"), cfg["model"], nx, nu, h_us, N,
                                      model=cfg["model"])
-        ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt]
+        ksolver = {"auto": 0, "condensed": 1, "riccati": 2, "group": 3}[args.kkt if primary else "auto"]
         solver = mmpc.Solver(path, device=local, kkt_solver=ksolver, factor_fp32=cfg["fp32"],
                              tol_grad=tol_grad, tol_defect=tol_defect,
                              init_states={"zero": mmpc.INIT_ZERO, "as_given": mmpc.INIT_AS_GIVEN,
                                           "hold_x0": mmpc.INIT_HOLD_X0}[args.init],
                              hessian={"auto": mmpc.HESSIAN_AUTO, "gauss_newton": mmpc.HESSIAN_GAUSS_NEWTON,
-                                      "exact": mmpc.HESSIAN_EXACT}[args.hessian])
+                                      "exact": mmpc.HESSIAN_EXACT}[args.hessian if primary else "auto"])
         solver.reserve_workspace(B)
         ksolver = solver.kkt_solver_for(B)   # the AUTO choice, resolved by the library
         hess = solver.hessian_for(B)
@@ -334,7 +382,9 @@ def run_rank(args):
     def hbytes(k):
         return torch.from_numpy(np.frombuffer(hbuf[k % 2]._buf, dtype=np.uint8).copy())
 
-    zc_ok = True
+    # zero-copy results check: None = unchecked (N > 1 needs two timed steps: the previous step's host buffer holds
+    # the same instances as the gathered last step)
+    zc_ok = None
     if zero_copy and world == 1:   # the host buffer of the last step IS the result table; check it against V
         hb = hviews[(args.steps - 1) % 2]
         res.copy_(hbytes(args.steps - 1))
@@ -343,13 +393,12 @@ def run_rank(args):
     elif zero_copy and args.steps >= 2:   # N > 1: the previous step (same instances) stored into host memory
         zc_ok = bool(torch.equal(hbytes(args.steps - 2), res.cpu()))
     iters = it.cpu().numpy()
-    status = st.cpu().numpy()
     # rank 0's host table of the last step against every rank's own results
     mine = res.cpu()
-    ok = zc_ok
+    ok = zc_ok is not False
     if rank == 0:
         last = host[(args.steps - 1) % 2]
-        ok = bool(torch.equal(last[:nbytes], mine)) and zc_ok
+        ok = bool(torch.equal(last[:nbytes], mine)) and ok
         conv = sum(int((last[r * nbytes + B * nu * 8:r * nbytes + B * nu * 8 + 4 * B].view(torch.int32) == 0).sum())
                    for r in range(world))
         tail = last
@@ -373,7 +422,7 @@ def run_rank(args):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64" if not cfg["fp32"] else "f64 (fp32 Riccati factor)",
-        "data": f"synthetic: counter-based splitmix64 {args.config} instances (SURVEY.md 8d), generated on device "
+        "data": f"synthetic: counter-based splitmix64 {name} instances (SURVEY.md 8d), generated on device "
                 f"from (seed, global instance index), so N = 1 and N > 1 solve identical instances",
         "config": {"workload": cfg["workload"], "batch_per_gpu": B, "global_batch": B * world,
                    "horizon": N, "tol_grad": tol_grad, "tol_defect": tol_defect,
@@ -392,9 +441,12 @@ def run_rank(args):
                                     + ("; the last step's table of all ranks on rank 0's host" if world > 1 else ""))},
         "converged": conv,
         "gathered_results_match": ok,
+        "zero_copy_results_checked": zc_ok is not None,
         "mean_sqp_iters": float(iters.mean()),
         "max_sqp_iters": int(iters.max()),
     }
+    if name == "cfg3" and world > 1:
+        out["config"]["workload"] = "cfg#4 (SURVEY.md 8d): " + cfg["workload"] + f", weak-scaled over {world} GPUs"
     if standin:
         out["standin"] = True
         if tail is not None:   # u_0*[:, 0] of every rank's slice of the gathered table
@@ -402,23 +454,19 @@ def run_rank(args):
                                            for v in tail[r * nbytes:r * nbytes + B * nu * 8].view(torch.float64)
                                            .view(B, nu)[:, 0].tolist()]
     else:
-        import mmpc
         out["kernel_ms"] = kern_ms
-        out["roofline"] = roofline(args, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms)
-    if args.config == "cfg5" and world == 1 and not standin:
+        out["roofline"] = roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms)
+    if name == "cfg5" and world == 1 and not standin and not args.no_sweep:
         out["tolerance_sweep"] = cfg5_sweep(path, cfg, B, x0, up, tr, w, args.hessian)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin and name != "cfg5":
         out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
                                            tol_defect, hess)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     if hbuf:
         for hb in hbuf:
             hb.close()
     if not standin:
         solver.close()
-    if world > 1:
-        dist.destroy_process_group()
+    return out
 
 
 def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3):
@@ -461,7 +509,7 @@ def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3):
     return rows
 
 
-def roofline(args, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms):
+def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms):
     """FP64-VALU roofline of the solve kernel (the only kernel of a step besides a memset and the result pack).
 
     achieved = the kernel's OWN algorithmic flop count (mmpc.*_flops_per_iteration: structure-exploiting, no
@@ -486,19 +534,27 @@ def roofline(args, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms):
     survey = float(iters.sum()) * mmpc.survey_flops_per_iteration(N, nx, nu) / sec / 1e12
     traffic = None
     traffic_src, pmc = None, {}
-    if os.path.exists(args.traffic_json):   # keyed "<config>:<kernel name prefix>"
+    sha = lib_sha256(os.path.realpath(mmpc.LIB_PATH))
+    pmc_status = "no PMC summary for this config/kernel"
+    if os.path.exists(args.traffic_json):   # keyed "<config>:<kernel name prefix>", tied to a library build
         try:
             for key, tj in json.load(open(args.traffic_json)).items():
-                if (key.startswith(f"{args.config}:{kname}") and isinstance(tj, dict) and tj.get("batch") == B
-                        and tj.get("horizon") == N and tj.get("kernel_ms_at_measurement") is not None
-                        and abs(tj["kernel_ms_at_measurement"] - kern_ms) <= 0.10 * kern_ms):
-                    traffic, traffic_src, pmc = tj.get("hbm_bytes_per_launch"), tj.get("source"), tj
+                if not (key.startswith(f"{name}:{kname}") and isinstance(tj, dict) and tj.get("batch") == B
+                        and tj.get("horizon") == N):
+                    continue
+                if tj.get("lib_sha256") != sha:
+                    pmc_status = f"PMC summary {tj.get('source')} measured another build ({tj.get('lib_sha256')})"
+                    continue
+                traffic, traffic_src, pmc = tj.get("hbm_bytes_per_launch"), tj.get("source"), tj
+                pmc_status = "PMC of this exact library build (sha256 match)"
         except (OSError, ValueError):
             traffic = None
     alg_bytes = B * (8 * (nx + nu + N * nx + 2 * (nx * (N + 1) + nu * N)) + 12)   # SURVEY.md 8d, per launch
     return {"bound": "fp64-valu", "achieved": own, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": own / FP64_PEAK_TFLOPS, "traffic": traffic,
             "traffic_source": traffic_src,
+            "lib_sha256": sha,
+            "pmc_status": pmc_status,
             "kernel": kname,
             "flops_per_iter_kernel_own_count": fl["total"],
             "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N, nx, nu),
@@ -513,8 +569,8 @@ def roofline(args, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms):
             "pmc_lds_bank_conflict_cycles_per_launch": pmc.get("lds_bank_conflict_cycles"),
             "pmc_valu_active_frac": pmc.get("valu_active_frac"),
             "note": "frac = the kernel's own algorithmic flops / FP64 vector peak (no kernel issues MFMA: DESIGN.md "
-                    "'Why no MFMA'); pmc_* = rocprofv3 counters of the same kernel (tools/pmc.sh) when they match "
-                    "this run's shape and kernel time: issued FP64 VALU lane-flops incl. inactive-lane slots"}
+                    "'Why no MFMA'); pmc_* = rocprofv3 counters (tools/pmc.sh) of the same kernel, shape and library "
+                    "build (lib_sha256): issued FP64 VALU lane-flops incl. inactive-lane slots"}
 
 
 def main():

@@ -1404,7 +1404,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             const double phit = XB ? fma(mu, ct, fma(-2.0 * mub, lt, Jt)) : fma(mu, ct, Jt);
             const double noise = 1.0 + fabs(phi0);
             if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise ||
-                (!XB && it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct))) {
+                (!XB && it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct, dJ, alpha))) {
                 accepted = true;
                 break;
             }

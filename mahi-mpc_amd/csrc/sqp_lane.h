@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             const double phit = XB ? fma(mu, ct, fma(-2.0 * mub, lt, Jt)) : fma(mu, ct, Jt);
             const double noise = 1.0 + fabs(phi0);
             if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise ||
-                (!XB && it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct))) {
+                (!XB && it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct, dJ, alpha))) {
                 accepted = true;
                 break;
             }

@@ -83,12 +83,17 @@ constexpr int kBoundPasses = 4;
 __device__ __forceinline__ double proj(double v, double lb, double ub) { return v < lb ? lb : (v > ub ? ub : v); }
 
 // First SQP iteration: IPOPT's filter acceptance (Waechter & Biegler 2006, eqs. (18)-(21); oracle
-// first_iter_filter_accepts).  Its filter then holds only theta_max = 1e4 max(1, theta_0) and the cold start is far
-// from feasible (no switching to Armijo), so a trial (J_t, theta_t = |c_t|_1) is taken when theta_t <= theta_max and
-// theta_t <= (1 - 1e-5) theta_0 or J_t <= J_0 - 1e-5 theta_0.  Later iterations use the l1-merit Armijo test alone.
-__device__ __forceinline__ bool first_iter_filter_accepts(double J0, double c0, double Jt, double ct) {
+// first_iter_filter_accepts).  Its filter then holds only theta_max = 1e4 max(1, theta_0).  When the iterate is far
+// from feasible (theta_0 > theta_min = 1e-4 max(1, theta_0), the cold start) or the switching condition (19) fails,
+// a trial (J_t, theta_t = |c_t|_1) is taken when theta_t <= theta_max and theta_t <= (1 - 1e-5) theta_0 or
+// J_t <= J_0 - 1e-5 theta_0.  A nearly feasible first iterate (a warm start) whose step satisfies the switching
+// condition alpha (-dJ)^s_phi > theta_0^s_theta (s_phi = 2.3, s_theta = 1.1, delta = 1) is an f-type iteration:
+// the Armijo test alone decides it, as every later iteration.
+__device__ __forceinline__ bool first_iter_filter_accepts(double J0, double c0, double Jt, double ct, double dJ,
+                                                          double alpha) {
     if (!(isfinite(Jt) && isfinite(ct))) return false;
     if (ct > 1e4 * fmax(1.0, c0)) return false;
+    if (c0 <= 1e-4 * fmax(1.0, c0) && dJ < 0.0 && alpha * pow(-dJ, 2.3) > pow(c0, 1.1)) return false;
     return ct <= (1.0 - 1e-5) * c0 || Jt <= J0 - 1e-5 * c0;
 }
 // bound values of |b| >= 1e19 are infinite (IPOPT's convention); NaN marks a free control in hold fields
@@ -901,7 +906,7 @@ __global__ __launch_bounds__(64, MMPC_WAVES_PER_SIMD) void sqp_wave_kernel(Solve
             // of roundoff.  Without this the test compares noise and alpha collapses.
             const double noise = 1.0 + fabs(phi0);
             if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise ||
-                (it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct))) {
+                (it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct, dJ, alpha))) {
                 accepted = true;
                 break;
             }

@@ -156,30 +156,3 @@ def solve_rank0_batch(solver, x0=None, u_prev=None, traj=None, weights=None, V=N
         return None
     return dict(V=full[:, :NV], status=full[:, NV].to(torch.int32), iters=full[:, NV + 1].to(torch.int32),
                 kkt=full[:, NV + 2])
-
-
-class ResultGather:
-    """Weak-scaled batches: after every solve, each rank's per-instance results -- u_0* (the control the
-    reference applies, ModelControl.cpp:174-190), status and iterations -- go to rank 0 in one async
-    all_gather_into_tensor (~100 KB per rank for cfg#2), so the exchange overlaps the next solve; ``wait``
-    joins all of them.  ``last()`` is the [world*B, nu+2] table of the latest step (instance-major)."""
-
-    def __init__(self, B: int, nx: int, nu: int):
-        import torch.distributed as dist
-        self.B, self.nx, self.nu = B, nx, nu
-        self.world = dist.get_world_size()
-        self.pending = []
-
-    def post(self, V, status, iters):
-        import torch
-        import torch.distributed as dist
-        pack = torch.cat([V[:, self.nx:self.nx + self.nu], status.double()[:, None], iters.double()[:, None]], 1)
-        out = torch.empty((self.world * self.B, self.nu + 2), dtype=torch.float64, device=V.device)
-        self.pending.append((dist.all_gather_into_tensor(out, pack, async_op=True), out, pack))
-
-    def wait(self):
-        for work, _, _ in self.pending:
-            work.wait()
-
-    def last(self):
-        return self.pending[-1][1] if self.pending else None

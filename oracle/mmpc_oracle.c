@@ -452,6 +452,7 @@ int oracle_nlp_hess(int model, int N, double h, const double* V, const double* u
 typedef struct {
     int N, M;
     double *X, *U, *F, *Ad, *Bd, *c, *d, *e, *G, *H, *g, *du, *dx, *lam, *Xt, *Ut, *Ft, *H0, *g0, *tgt;
+    double *Kf, *Wk;  /* Riccati variant: [K_k | kff_k] per stage, exact-Hessian stage blocks W_k */
 } ws_t;
 
 static void ws_alloc(ws_t* s, int N) {
@@ -477,11 +478,14 @@ static void ws_alloc(ws_t* s, int N) {
     s->H0 = calloc(M * M, sizeof(double));
     s->g0 = calloc(M, sizeof(double));
     s->tgt = calloc(M, sizeof(double));
+    s->Kf = calloc((size_t)N * NU * (NX + NU + 1), sizeof(double));
+    s->Wk = calloc((size_t)N * (NX + NU) * (NX + NU), sizeof(double));
 }
 static void ws_free(ws_t* s) {
     free(s->X); free(s->U); free(s->F); free(s->Ad); free(s->Bd); free(s->c); free(s->d);
     free(s->e); free(s->G); free(s->H); free(s->g); free(s->du); free(s->dx); free(s->lam);
     free(s->Xt); free(s->Ut); free(s->Ft); free(s->H0); free(s->g0); free(s->tgt);
+    free(s->Kf); free(s->Wk);
 }
 
 /* merit pieces at (X,U): J and sum |c| (F returned) */
@@ -533,10 +537,15 @@ static int chol_solve(int M, double* H, double* b /* in: rhs, out: solution */) 
 
 /* IPOPT's filter acceptance of a trial (J_t, theta_t = |c_t|_1) w.r.t. the first iterate (J_0, theta_0) -- the
  * filter holds only (theta_max, -inf) then: theta_t <= theta_max = 1e4 max(1, theta_0), and theta_t <= (1 - 1e-5)
- * theta_0 or J_t <= J_0 - 1e-5 theta_0 (gamma_theta = gamma_phi = 1e-5).  J-scale as the merit. */
-static int first_iter_filter_accepts(double J0, double c0, double Jt, double ct) {
+ * theta_0 or J_t <= J_0 - 1e-5 theta_0 (gamma_theta = gamma_phi = 1e-5).  J-scale as the merit.
+ * That test applies when the first iterate is far from feasible (theta_0 > theta_min = 1e-4 max(1, theta_0): the
+ * reference's cold start) or the switching condition of Waechter & Biegler (2006) eq. (19) fails.  A nearly feasible
+ * first iterate (a warm start) whose step satisfies alpha (-dJ)^s_phi > delta theta_0^s_theta (s_phi = 2.3,
+ * s_theta = 1.1, delta = 1; dJ the directional derivative of J) is an f-type iteration: Armijo alone decides. */
+int oracle_first_iter_filter_accepts(double J0, double c0, double Jt, double ct, double dJ, double alpha) {
     if (!(isfinite(Jt) && isfinite(ct))) return 0;
     if (ct > 1e4 * fmax(1.0, c0)) return 0;
+    if (c0 <= 1e-4 * fmax(1.0, c0) && dJ < 0.0 && alpha * pow(-dJ, 2.3) > pow(c0, 1.1)) return 0;
     return ct <= (1.0 - 1e-5) * c0 || Jt <= J0 - 1e-5 * c0;
 }
 
@@ -808,7 +817,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
             /* first iteration: IPOPT's filter acceptance (Waechter & Biegler 2006, eqs. (18)-(21)) -- its filter then
              * holds only theta_max = 1e4 max(1, theta_0), the cold start is far from feasible (no switching), so a
              * trial is taken when it reduces the constraint violation or the objective sufficiently */
-            if (it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct)) { accepted = 1; break; }
+            if (it == 0 && oracle_first_iter_filter_accepts(J0, c1, Jt, ct, dJ, alpha)) { accepted = 1; break; }
             alpha *= 0.5;
         }
         if (!accepted) { status = ORACLE_LINESEARCH_FAILED; break; }
@@ -816,6 +825,295 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         memcpy(s->U, s->Ut, sizeof(double) * M);
     }
     /* pack V */
+    for (int k = 0; k < N; ++k) {
+        memcpy(V + k * ND, s->X + k * NX, sizeof(double) * NX);
+        memcpy(V + k * ND + NX, s->U + k * NU, sizeof(double) * NU);
+    }
+    memcpy(V + N * ND, s->X + N * NX, sizeof(double) * NX);
+    if (J_out) {
+        double J;
+        oracle_nlp_eval(t_model, N, h, V, u_prev, traj, w, &J, NULL);
+        *J_out = J;
+    }
+    *iters_out = it;
+    *kkt_out = kkt;
+    return status;
+}
+
+/* ---------------- the same SQP with a Riccati KKT solve (ORACLE_KKT_RICCATI) ----------------
+ * The HIP kernels solve each QP by a Riccati recursion on the augmented state s_k = [dx_k; du_{k-1}] (NS = nx + nu;
+ * du_{k-1} carries the Delta-u weight of ModelGenerator.cpp:216-221) instead of condensing.  This restates that
+ * formulation on the CPU -- stage evaluation, propagated defects d, adjoint lam and reduced gradient (stop test),
+ * exact-Hessian stage blocks, backward Riccati sweep, forward step, l1-merit line search -- so that the CPU
+ * baseline of bench.py runs the algorithm the GPU runs (cpu_baseline.riccati).  Same NLP, iterates and stop test
+ * as solve_one (the QP solution is identical up to roundoff); unbounded nonlinear solves only.  O(N (nx+nu)^3)
+ * per iteration against solve_one's O((N nu)^3). */
+static int g_kkt_mode = ORACLE_KKT_DENSE;
+void oracle_set_kkt(int mode) { g_kkt_mode = mode; }
+
+/* Cholesky of the nu x nu stage matrix Hw (lower factor in place); -1 if not positive definite */
+static int small_chol(int n, double* Hw) {
+    for (int j = 0; j < n; ++j) {
+        double sd = Hw[j * n + j];
+        for (int q = 0; q < j; ++q) sd -= Hw[j * n + q] * Hw[j * n + q];
+        if (!(sd > 0.0) || !isfinite(sd)) return -1;
+        const double l = sqrt(sd);
+        Hw[j * n + j] = l;
+        for (int i = j + 1; i < n; ++i) {
+            double t = Hw[i * n + j];
+            for (int q = 0; q < j; ++q) t -= Hw[i * n + q] * Hw[j * n + q];
+            Hw[i * n + j] = t / l;
+        }
+    }
+    return 0;
+}
+/* x = Hw^-1 b with the factor of small_chol */
+static void small_chol_solve(int n, const double* L, const double* b, double* x) {
+    double y[ORACLE_MAX_NU];
+    for (int i = 0; i < n; ++i) {
+        double t = b[i];
+        for (int q = 0; q < i; ++q) t -= L[i * n + q] * y[q];
+        y[i] = t / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double t = y[i];
+        for (int q = i + 1; q < n; ++q) t -= L[q * n + i] * x[q];
+        x[i] = t / L[i * n + i];
+    }
+}
+
+/* backward Riccati sweep of the QP at the current iterate (J/2 scale): value function 1/2 s^T P s + p^T s of
+ * s_k = [dx_k; du_{k-1}], P_N = blkdiag(Q, 0), p_N = [Q (x_N - r_{N-1}); 0]; per stage k
+ *   Q_uu = [B;I]^T P [B;I] + R + Rm (+ W_uu),   Q_us = [G^T A (+ W_ux) | -R],  G = P_xx B + P_xu,
+ *   q_u  = B^T (P_xx c + p_x) + P_ux c + p_u + R (u_k - u_{k-1}) + Rm u_k,
+ *   [K_k | kff_k] = -Q_uu^-1 [Q_us | q_u],
+ *   P_k = blkdiag(A^T P_xx A + Q (+ W_xx), R) - Q_us^T Q_uu^-1 Q_us,
+ *   p_k = [A^T (P_xx c + p_x) + Q (x_k - r_{k-1}); -R (u_k - u_{k-1})] - Q_us^T Q_uu^-1 q_u.
+ * useW: add the exact-Hessian blocks s->Wk.  Returns -1 when a Q_uu is not positive definite. */
+static int riccati_backward(ws_t* s, const double* traj, const double* w, const double* u_prev, int useW) {
+    const int N = s->N, NS = NX + NU, K = NX + NU;
+    const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
+    double P[(ORACLE_MAX_NX + ORACLE_MAX_NU) * (ORACLE_MAX_NX + ORACLE_MAX_NU)], p[ORACLE_MAX_NX + ORACLE_MAX_NU];
+    double Pn[(ORACLE_MAX_NX + ORACLE_MAX_NU) * (ORACLE_MAX_NX + ORACLE_MAX_NU)], pn[ORACLE_MAX_NX + ORACLE_MAX_NU];
+    for (int i = 0; i < NS * NS; ++i) P[i] = 0.0;
+    for (int r = 0; r < NX; ++r) {
+        P[r * NS + r] = Q[r];
+        p[r] = Q[r] * (s->X[N * NX + r] - traj[(N - 1) * NX + r]);
+    }
+    for (int c = 0; c < NU; ++c) p[NX + c] = 0.0;
+    for (int k = N - 1; k >= 0; --k) {
+        const double *A = s->Ad + (size_t)k * NX * NX, *Bm = s->Bd + (size_t)k * NX * NU, *cc = s->c + k * NX;
+        const double* u = s->U + k * NU;
+        const double* um = (k == 0) ? u_prev : s->U + (k - 1) * NU;
+        const double* Wk = s->Wk + (size_t)k * K * K;
+        double G[ORACLE_MAX_NX * ORACLE_MAX_NU], mv[ORACLE_MAX_NX], Hw[ORACLE_MAX_NU * ORACLE_MAX_NU];
+        double Y[ORACLE_MAX_NU * (ORACLE_MAX_NX + ORACLE_MAX_NU + 1)];   /* [Q_us | q_u], NU x (NS + 1) */
+        for (int r = 0; r < NX; ++r) {
+            for (int c = 0; c < NU; ++c) {
+                double t = P[r * NS + NX + c];
+                for (int q = 0; q < NX; ++q) t += P[r * NS + q] * Bm[q * NU + c];
+                G[r * NU + c] = t;
+            }
+            double t = p[r];
+            for (int q = 0; q < NX; ++q) t += P[r * NS + q] * cc[q];
+            mv[r] = t;
+        }
+        for (int a = 0; a < NU; ++a) {
+            for (int b = 0; b < NU; ++b) {
+                double t = P[(NX + a) * NS + NX + b];
+                for (int q = 0; q < NX; ++q) t += Bm[q * NU + a] * G[q * NU + b] + P[(NX + a) * NS + q] * Bm[q * NU + b];
+                if (a == b) t += R[a] + Rm[a];
+                if (useW) t += Wk[(NX + a) * K + NX + b];
+                Hw[a * NU + b] = t;
+            }
+            double* y = Y + a * (NS + 1);
+            for (int j = 0; j < NX; ++j) {   /* (G^T A)[a][j] (+ W_ux) */
+                double t = 0.0;
+                for (int q = 0; q < NX; ++q) t += G[q * NU + a] * A[q * NX + j];
+                if (useW) t += Wk[(NX + a) * K + j];
+                y[j] = t;
+            }
+            for (int c = 0; c < NU; ++c) y[NX + c] = (a == c) ? -R[a] : 0.0;
+            double t = p[NX + a] + R[a] * (u[a] - um[a]) + Rm[a] * u[a];
+            for (int q = 0; q < NX; ++q) t += Bm[q * NU + a] * mv[q] + P[(NX + a) * NS + q] * cc[q];
+            y[NS] = t;
+        }
+        if (small_chol(NU, Hw) != 0) return -1;
+        double* Kk = s->Kf + (size_t)k * NU * (NS + 1);   /* row a: K_k[a][0..NS), kff_k[a] */
+        for (int j = 0; j <= NS; ++j) {
+            double col[ORACLE_MAX_NU], sol[ORACLE_MAX_NU];
+            for (int a = 0; a < NU; ++a) col[a] = Y[a * (NS + 1) + j];
+            small_chol_solve(NU, Hw, col, sol);
+            for (int a = 0; a < NU; ++a) Kk[a * (NS + 1) + j] = -sol[a];
+        }
+        if (k == 0) break;
+        /* P_k, p_k before the Schur complement */
+        for (int i = 0; i < NS * NS; ++i) Pn[i] = 0.0;
+        for (int i = 0; i < NX; ++i) {
+            for (int j = 0; j < NX; ++j) {
+                double t = 0.0;
+                for (int q = 0; q < NX; ++q) {
+                    double pa = 0.0;
+                    for (int r = 0; r < NX; ++r) pa += P[q * NS + r] * A[r * NX + j];
+                    t += A[q * NX + i] * pa;
+                }
+                if (i == j) t += Q[i];
+                if (useW) t += Wk[i * K + j];
+                Pn[i * NS + j] = t;
+            }
+            double t = Q[i] * (s->X[k * NX + i] - traj[(k - 1) * NX + i]);
+            for (int q = 0; q < NX; ++q) t += A[q * NX + i] * mv[q];
+            pn[i] = t;
+        }
+        for (int c = 0; c < NU; ++c) {
+            Pn[(NX + c) * NS + NX + c] = R[c];
+            pn[NX + c] = -R[c] * (u[c] - um[c]);
+        }
+        /* - Q_us^T Q_uu^-1 [Q_us | q_u] = + Q_us^T [K | kff] */
+        for (int i = 0; i < NS; ++i) {
+            for (int j = 0; j < NS; ++j) {
+                double t = Pn[i * NS + j];
+                for (int a = 0; a < NU; ++a) t += Y[a * (NS + 1) + i] * Kk[a * (NS + 1) + j];
+                P[i * NS + j] = t;
+            }
+            double t = pn[i];
+            for (int a = 0; a < NU; ++a) t += Y[a * (NS + 1) + i] * Kk[a * (NS + 1) + NS];
+            p[i] = t;
+        }
+        for (int i = 0; i < NS; ++i)   /* symmetric by construction up to roundoff: keep it exactly symmetric */
+            for (int j = i + 1; j < NS; ++j) P[j * NS + i] = P[i * NS + j] = 0.5 * (P[i * NS + j] + P[j * NS + i]);
+    }
+    return 0;
+}
+
+static int solve_one_riccati(ws_t* s, double h, const double* x0, const double* u_prev, const double* traj,
+                             const double* w, int max_iter, double tol_grad, double tol_defect, double* V,
+                             int32_t* iters_out, double* kkt_out, double* J_out) {
+    const int N = s->N, M = s->M, K = NX + NU, NS = NX + NU;
+    const double *Q = w, *R = w + NX, *Rm = w + NX + NU;
+    for (int k = 0; k < N; ++k) {
+        memcpy(s->X + k * NX, V + k * ND, sizeof(double) * NX);
+        memcpy(s->U + k * NU, V + k * ND + NX, sizeof(double) * NU);
+    }
+    memcpy(s->X + N * NX, V + N * ND, sizeof(double) * NX);
+    if (g_init_zero) {
+        memset(s->X, 0, sizeof(double) * (N + 1) * NX);
+        memset(s->U, 0, sizeof(double) * N * NU);
+    }
+    memcpy(s->X, x0, sizeof(double) * NX);
+    if (g_init_hold)
+        for (int k = 1; k <= N; ++k) memcpy(s->X + k * NX, x0, sizeof(double) * NX);
+    const int use_exact = g_hess_mode == ORACLE_HESS_EXACT && !g_lin && model_has_hess();
+    int status = ORACLE_MAX_ITER, it = 0;
+    double kkt = INFINITY, mu = 0.0;
+    for (it = 0; it <= max_iter; ++it) {
+        double cmax = 0.0;
+        for (int k = 0; k < N; ++k)
+            euler_step(h, s->X + k * NX, s->U + k * NU, s->F + k * NX, s->Ad + (size_t)k * NX * NX,
+                       s->Bd + (size_t)k * NX * NU);
+        for (int i = 0; i < N * NX; ++i) {
+            s->c[i] = s->F[i] - s->X[NX + i];
+            if (fabs(s->c[i]) > cmax || s->c[i] != s->c[i]) cmax = fabs(s->c[i]);
+        }
+        /* propagated defects d and the adjoint of the condensed objective (J/2 scale) */
+        memset(s->d, 0, sizeof(double) * NX);
+        for (int k = 0; k < N; ++k)
+            for (int r = 0; r < NX; ++r) {
+                double t = s->c[k * NX + r];
+                for (int q = 0; q < NX; ++q) t += s->Ad[(size_t)k * NX * NX + r * NX + q] * s->d[k * NX + q];
+                s->d[(k + 1) * NX + r] = t;
+            }
+        double lmax = 0.0;
+        for (int r = 0; r < NX; ++r) {
+            s->lam[N * NX + r] = Q[r] * (s->d[N * NX + r] + s->X[N * NX + r] - traj[(N - 1) * NX + r]);
+            if (fabs(s->lam[N * NX + r]) > lmax) lmax = fabs(s->lam[N * NX + r]);
+        }
+        for (int k = N - 1; k >= 1; --k)
+            for (int r = 0; r < NX; ++r) {
+                double t = Q[r] * (s->d[k * NX + r] + s->X[k * NX + r] - traj[(k - 1) * NX + r]);
+                for (int q = 0; q < NX; ++q) t += s->Ad[(size_t)k * NX * NX + q * NX + r] * s->lam[(k + 1) * NX + q];
+                s->lam[k * NX + r] = t;
+                if (fabs(t) > lmax) lmax = fabs(t);
+            }
+        double gmax = 0.0;
+        for (int k = 0; k < N; ++k)
+            for (int c = 0; c < NU; ++c) {
+                double g = 0.0;
+                for (int q = 0; q < NX; ++q) g += s->Bd[(size_t)k * NX * NU + q * NU + c] * s->lam[(k + 1) * NX + q];
+                const double uk = s->U[k * NU + c], um = (k == 0) ? u_prev[c] : s->U[(k - 1) * NU + c];
+                g += R[c] * (uk - um) + Rm[c] * uk;
+                if (k + 1 < N) g -= R[c] * (s->U[(k + 1) * NU + c] - uk);
+                const double t = fabs(2.0 * g);
+                if (t > gmax || t != t) gmax = t;
+            }
+        kkt = gmax > cmax ? gmax : cmax;
+        if (!isfinite(kkt)) { status = ORACLE_NONFINITE; break; }
+        if (gmax <= tol_grad && cmax <= tol_defect) { status = ORACLE_CONVERGED; break; }
+        if (it == max_iter) { status = ORACLE_MAX_ITER; break; }
+        if (use_exact)   /* W_k = h sum_r lam_{k+1,r} d^2 f_r/d(x_k,u_k)^2 */
+            for (int k = 0; k < N; ++k) {
+                double* Wk = s->Wk + (size_t)k * K * K;
+                model_hess(s->X + k * NX, s->U + k * NU, s->lam + (k + 1) * NX, Wk);
+                for (int i = 0; i < K * K; ++i) Wk[i] *= h;
+            }
+        int rc = riccati_backward(s, traj, w, u_prev, use_exact);
+        if (rc != 0 && use_exact) rc = riccati_backward(s, traj, w, u_prev, 0);   /* not PD: Gauss-Newton step */
+        if (rc != 0) { status = ORACLE_FACTORIZATION_FAILED; break; }
+        /* forward: du_k = K_k [dx_k; du_{k-1}] + kff_k, dx_{k+1} = A dx_k + B du_k + c_k */
+        memset(s->dx, 0, sizeof(double) * NX);
+        for (int k = 0; k < N; ++k) {
+            const double* Kk = s->Kf + (size_t)k * NU * (NS + 1);
+            for (int a = 0; a < NU; ++a) {
+                double t = Kk[a * (NS + 1) + NS];
+                for (int q = 0; q < NX; ++q) t += Kk[a * (NS + 1) + q] * s->dx[k * NX + q];
+                if (k > 0)
+                    for (int c = 0; c < NU; ++c) t += Kk[a * (NS + 1) + NX + c] * s->du[(k - 1) * NU + c];
+                s->du[k * NU + a] = t;
+            }
+            for (int r = 0; r < NX; ++r) {
+                double t = s->c[k * NX + r];
+                for (int q = 0; q < NX; ++q) t += s->Ad[(size_t)k * NX * NX + r * NX + q] * s->dx[k * NX + q];
+                for (int q = 0; q < NU; ++q) t += s->Bd[(size_t)k * NX * NU + r * NU + q] * s->du[k * NU + q];
+                s->dx[(k + 1) * NX + r] = t;
+            }
+        }
+        /* l1-merit Armijo line search, as solve_one */
+        double mu_new = 4.0 * lmax + 1.0;
+        if (mu_new > mu) mu = mu_new;
+        double J0 = 0.0, c1 = 0.0, dJ = 0.0;
+        for (int k = 0; k < N; ++k) {
+            for (int r = 0; r < NX; ++r) {
+                const double e = s->F[k * NX + r] - traj[k * NX + r];
+                J0 += e * Q[r] * e;
+                c1 += fabs(s->c[k * NX + r]);
+                double ad = s->dx[(k + 1) * NX + r] - s->c[k * NX + r];   /* A dx_k + B du_k */
+                dJ += 2.0 * Q[r] * e * ad;
+            }
+            for (int q = 0; q < NU; ++q) {
+                const double um = (k == 0) ? u_prev[q] : s->U[(k - 1) * NU + q];
+                const double dum = (k == 0) ? 0.0 : s->du[(k - 1) * NU + q];
+                const double uk = s->U[k * NU + q], dif = uk - um;
+                J0 += dif * R[q] * dif + uk * Rm[q] * uk;
+                dJ += 2.0 * R[q] * dif * (s->du[k * NU + q] - dum) + 2.0 * Rm[q] * uk * s->du[k * NU + q];
+            }
+        }
+        const double phi0 = J0 + mu * c1, dphi = dJ - mu * c1;
+        double alpha = 1.0;
+        int accepted = 0;
+        for (int ls = 0; ls < 30; ++ls) {
+            for (int i = 0; i < (N + 1) * NX; ++i) s->Xt[i] = s->X[i] + alpha * s->dx[i];
+            for (int i = 0; i < M; ++i) s->Ut[i] = s->U[i] + alpha * s->du[i];
+            double Jt, ct;
+            merit_eval(N, h, s->Xt, s->Ut, u_prev, traj, w, s->Ft, &Jt, &ct);
+            const double phit = Jt + mu * ct, noise = 1.0 + fabs(phi0);
+            if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) { accepted = 1; break; }
+            if (it == 0 && oracle_first_iter_filter_accepts(J0, c1, Jt, ct, dJ, alpha)) { accepted = 1; break; }
+            alpha *= 0.5;
+        }
+        if (!accepted) { status = ORACLE_LINESEARCH_FAILED; break; }
+        memcpy(s->X, s->Xt, sizeof(double) * (N + 1) * NX);
+        memcpy(s->U, s->Ut, sizeof(double) * M);
+    }
     for (int k = 0; k < N; ++k) {
         memcpy(V + k * ND, s->X + k * NX, sizeof(double) * NX);
         memcpy(V + k * ND + NX, s->U + k * NU, sizeof(double) * NU);
@@ -1165,6 +1463,8 @@ int oracle_solve_batch_xb(int model, int is_linear, int N, double h, int64_t B, 
     int x_bounded = 0;
     for (int r = 0; r < NX; ++r) x_bounded |= (x_lb && x_lb[r] > -1e19) || (x_ub && x_ub[r] < 1e19);
     const int NV = NX * (N + 1) + NU * N;
+    int u_b = 0;   /* finite control bounds (the Riccati variant covers unbounded solves only) */
+    for (int c = 0; c < NU; ++c) u_b |= (u_lb && u_lb[c] > -1e19) || (u_ub && u_ub[c] < 1e19);
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
 #else
@@ -1193,6 +1493,10 @@ int oracle_solve_batch_xb(int model, int is_linear, int N, double h, int64_t B, 
                 status[b] = solve_one_ip(&s, h, x0 + b * NX, u_prev + b * NU, traj + b * (int64_t)N * NX,
                                          weights + b * w_stride, u_lb, u_ub, x_lb, x_ub, max_iter, tol_grad,
                                          tol_defect, V + b * NV, &it, &kk, &J);
+            else if (g_kkt_mode == ORACLE_KKT_RICCATI && !is_linear && !u_b)
+                status[b] = solve_one_riccati(&s, h, x0 + b * NX, u_prev + b * NU, traj + b * (int64_t)N * NX,
+                                              weights + b * w_stride, max_iter, tol_grad, tol_defect, V + b * NV,
+                                              &it, &kk, &J);
             else
                 status[b] = solve_one(&s, h, x0 + b * NX, u_prev + b * NU, traj + b * (int64_t)N * NX,
                                       weights + b * w_stride, u_lb, u_ub, max_iter, tol_grad, tol_defect,

@@ -112,6 +112,15 @@ int oracle_solve_batch_xb(int model, int is_linear, int N, double h, int64_t B, 
                           int max_iter, double tol_grad, double tol_defect, double* V, int32_t* status,
                           int32_t* iters, double* kkt, double* Jout, int nthreads);
 
+/* the first SQP iteration's line-search acceptance (IPOPT's filter with theta_min and the switching condition,
+ * Waechter & Biegler 2006 eqs. (18)-(21)); 1 = accept.  The kernels run the same rule (sqp_wave.h). */
+int oracle_first_iter_filter_accepts(double J0, double c0, double Jt, double ct, double dJ, double alpha);
+
+/* KKT solve of the following unbounded nonlinear solves (process-wide): ORACLE_KKT_DENSE (explicit condensing +
+ * Cholesky, the default) or ORACLE_KKT_RICCATI (the Riccati recursion the HIP kernels run, same iterates) */
+enum { ORACLE_KKT_DENSE = 0, ORACLE_KKT_RICCATI = 1 };
+void oracle_set_kkt(int mode);
+
 /* mmpc_opts.init_states for the following solves (process-wide): 0 = V as given, 1 = x_1..x_N start at x_0,
  * 2 = V taken as zero (MMPC_INIT_ZERO) */
 void oracle_set_init_states(int mode);

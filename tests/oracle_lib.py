@@ -18,6 +18,7 @@ LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
 NX, NU = 4, 2                       # 2-link arm (model 0)
 TWO_LINK, EXO, USER = 0, 1, 2
 HESS_GAUSS_NEWTON, HESS_EXACT = 0, 1   # oracle_set_hessian (mmpc_opts.hessian after resolution)
+KKT_DENSE, KKT_RICCATI = 0, 1          # oracle_set_kkt: explicit condensing + Cholesky, or the kernels' Riccati
 DIMS = {TWO_LINK: (4, 2), EXO: (8, 4)}
 USER_DIR = os.path.join(ORACLE_DIR, "_user")
 _lib = None
@@ -59,6 +60,7 @@ def lib():
         L.oracle_exo_mass.argtypes = [_dp, _dp]
         L.oracle_two_link_hess.argtypes = [_dp, _dp, _dp, _dp]
         L.oracle_set_hessian.argtypes = [C.c_int]
+        L.oracle_set_kkt.argtypes = [C.c_int]
         L.oracle_nlp_hess.argtypes = [C.c_int, C.c_int, C.c_double, _dp, _dp, _dp, _dp, C.c_double, C.c_void_p, _dp]
         L.oracle_nlp_hess.restype = C.c_int
         _lib = L
@@ -197,21 +199,24 @@ def synth(seed, first, B, N, h, model=TWO_LINK):
 
 def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=200,
                 tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK, x_lb=None, x_ub=None,
-                init_states=0, hessian=HESS_GAUSS_NEWTON, solver=None):
+                init_states=0, hessian=HESS_GAUSS_NEWTON, solver=None, kkt=KKT_DENSE):
     """solver: the GPU mmpc.Solver being checked -- the oracle then runs the Hessian that solver resolves for this
-    batch (mmpc_resolve_hessian: exact for unbounded 2-link / generated-model solves on the group kernel)."""
+    batch (mmpc_resolve_hessian: exact for unbounded 2-link / generated-model solves on the group kernel).
+    kkt: KKT_DENSE (default; explicit condensing) or KKT_RICCATI (the kernels' recursion; unbounded solves)."""
     if solver is not None:
         fin = lambda b: b is not None and bool((np.abs(np.asarray(b, dtype=np.float64)) < 1e19).any())  # noqa: E731
         hessian = {1: HESS_GAUSS_NEWTON, 2: HESS_EXACT}[solver.hessian_for(int(np.asarray(x0).reshape(-1, DIMS[model][0]).shape[0]),
                                                                           fin(u_lb) or fin(u_ub))]
     lib().oracle_set_init_states(int(init_states))
     lib().oracle_set_hessian(int(hessian))
+    lib().oracle_set_kkt(int(kkt))
     try:
         return _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_grad, tol_defect, nthreads,
                             is_linear, model, x_lb, x_ub)
     finally:
         lib().oracle_set_init_states(0)
         lib().oracle_set_hessian(HESS_GAUSS_NEWTON)
+        lib().oracle_set_kkt(KKT_DENSE)
 
 
 def _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_grad, tol_defect, nthreads,

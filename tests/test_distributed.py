@@ -119,16 +119,13 @@ def _rank0_worker(rank, world, port, q):
         else:
             r = mdist.solve_rank0_batch(solver)
         out.append(None if r is None else {k: v.numpy().copy() for k, v in r.items()})
-    # ResultGather: weak-scaled per-step results to rank 0
-    Bw = 5
-    g = mdist.ResultGather(Bw, 4, 2)
-    for step in range(2):
-        V = torch.arange(Bw * 10, dtype=torch.float64).reshape(Bw, 10) + 1000 * rank + 100 * step
-        g.post(V, torch.full((Bw,), rank, dtype=torch.int32), torch.full((Bw,), step, dtype=torch.int32))
-    g.wait()
-    last = g.last().numpy().copy()
+    # gather_rows: ragged rank-major rows to rank 0 (the results leg of solve_rank0_batch)
+    total = sum(r + 2 for r in range(world))
+    lo, n = mdist.shard_strong(total, rank, world)
+    mine = (torch.arange(total, dtype=torch.float64)[lo:lo + n, None] * 10)
+    last = mdist.gather_rows(mine, total)
     if rank == 0:
-        q.put((out, last))
+        q.put((out, last.numpy().copy()))
     dist.destroy_process_group()
 
 
@@ -157,9 +154,6 @@ def test_rank0_batch_scatter_solve_gather(world, oracle):
         np.testing.assert_array_equal(got["V"], ref["V"])
         np.testing.assert_array_equal(got["status"], ref["status"])
         np.testing.assert_array_equal(got["iters"], ref["iters"])
-    # ResultGather: rank-major rows of (u_0*, status, iters) of the last step
-    assert last.shape == (world * 5, 4)
-    for r in range(world):
-        rows = last[r * 5:(r + 1) * 5]
-        np.testing.assert_array_equal(rows[:, :2], (np.arange(50).reshape(5, 10) + 1000 * r + 100)[:, 4:6])
-        assert (rows[:, 2] == r).all() and (rows[:, 3] == 1).all()
+    # gather_rows: every rank's shard_strong rows, in global order, on rank 0
+    total = sum(r + 2 for r in range(world))
+    np.testing.assert_array_equal(last[:, 0], np.arange(total) * 10.0)

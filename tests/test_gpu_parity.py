@@ -248,3 +248,31 @@ def test_nonfinite_and_max_iter(model_json, mmpc_mod, oracle):
     o2 = oracle.solve_batch(30, H, x0[[0, 3]], up[[0, 3]], tr[[0, 3]], np.array(WEIGHTS_CFG), max_iter=1, solver=s2)
     assert (r2["status"] == 1).all() and (r2["iters"] == 1).all()
     assert _rel(r2["V"], o2["V"]).max() < 1e-9
+
+
+def test_warm_start_perturbed_state(model_json, mmpc_mod, oracle):
+    """The reference's steady-state tick (ModelControl.cpp:144-145,160-161): warm start from the previous solution
+    with a slightly moved measured state.  theta_0 is then below IPOPT's theta_min, so the first iteration is an
+    Armijo (f-type) one in the kernels as in the oracle (sqp_wave.h first_iter_filter_accepts); GPU = oracle, and
+    the first accepted step does not increase the constraint violation."""
+    N, B = 30, 256
+    x0, up, tr = oracle.synth(20250213, 300, B, N, H)
+    w = np.array(WEIGHTS_CFG)
+    s = mmpc_mod.Solver(model_json(N=N))
+    r1 = s.solve_batch_host(x0, up, tr, w)
+    assert (r1["status"] == 0).all()
+    x0p = x0 + np.random.default_rng(5).uniform(-1e-7, 1e-7, x0.shape)
+    Vw = r1["V"].copy()
+    Vw[:, :4] = x0p
+    g = s.solve_batch_host(x0p, up, tr, w, V=Vw)
+    o = oracle.solve_batch(N, H, x0p, up, tr, w, V=Vw, solver=s)
+    assert (g["status"] == 0).all()
+    _compare(g, o)
+    s1 = mmpc_mod.Solver(model_json(N=N), max_iter=1)
+    g1 = s1.solve_batch_host(x0p, up, tr, w, V=Vw)
+    o1 = oracle.solve_batch(N, H, x0p, up, tr, w, V=Vw, max_iter=1, solver=s1)
+    assert _rel(g1["V"], o1["V"]).max() < 1e-9
+    for b in range(0, B, 17):
+        _, c0 = oracle.nlp_eval(N, H, Vw[b], up[b], tr[b], w)
+        _, c1 = oracle.nlp_eval(N, H, g1["V"][b], up[b], tr[b], w)
+        assert np.abs(c1).sum() <= np.abs(c0).sum() <= 1e-4

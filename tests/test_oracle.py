@@ -173,3 +173,68 @@ def test_exact_hessian_same_kkt_point_fewer_iterations(oracle):
     for b in range(0, 512, 97):   # exact single-shooting stationarity of the exact-Hessian solutions
         U = ex["V"][b].reshape(-1)[[6 * k + 4 + c for k in range(N) for c in range(2)]]
         assert np.abs(oracle.reduced_gradient(N, h, x0[b], U, up[b], tr[b], w)).max() < 1e-7
+
+
+def test_first_iteration_filter_rule(oracle):
+    """IPOPT's first-iteration filter (Waechter & Biegler 2006, eqs. (18)-(21)): far from feasible (the cold start,
+    theta_0 > theta_min = 1e-4 max(1, theta_0)) a trial that lowers J sufficiently is taken even when |c|_1 rises
+    (up to theta_max); nearly feasible (a warm start) with the switching condition alpha (-dJ)^2.3 > theta_0^1.1
+    met, it is not -- the Armijo test alone decides that iteration."""
+    import ctypes as C
+    f = oracle.lib().oracle_first_iter_filter_accepts
+    f.argtypes = [C.c_double] * 6
+    f.restype = C.c_int
+    # cold start: theta_0 = 5
+    assert f(100.0, 5.0, 90.0, 7.0, -50.0, 1.0) == 1     # J decreased, theta rose within theta_max
+    assert f(100.0, 5.0, 101.0, 4.0, -50.0, 1.0) == 1    # theta decreased
+    assert f(100.0, 5.0, 101.0, 6.0, -50.0, 1.0) == 0    # neither
+    assert f(100.0, 5.0, 10.0, 6e4, -50.0, 1.0) == 0     # beyond theta_max = 1e4 max(1, theta_0)
+    assert f(100.0, 5.0, math.nan, 1.0, -50.0, 1.0) == 0
+    # warm start: theta_0 = 1e-9 <= theta_min and the switching condition holds -> f-type (Armijo only)
+    assert f(100.0, 1e-9, 90.0, 1e-3, -50.0, 1.0) == 0
+    assert f(100.0, 1e-9, 90.0, 1e-3, -50.0, 2.0 ** -20) == 0
+    # nearly feasible but no descent direction for J: the switching condition fails, the filter test applies
+    assert f(100.0, 1e-9, 90.0, 1e-3, 0.0, 1.0) == 1
+
+
+def test_warm_start_perturbed_first_step_keeps_feasibility(oracle):
+    """The reference's steady-state tick: warm start from the previous solution with a slightly moved measured
+    state (ModelControl.cpp:144-145,160-161).  theta_0 is then tiny, so the first iteration is an Armijo
+    (f-type) one: the accepted step must not increase the constraint violation, and the solve converges."""
+    N, h = 30, 0.002
+    x0, up, tr = oracle.synth(20250213, 300, 64, N, h)
+    w = np.array(WEIGHTS_CFG)
+    r1 = oracle.solve_batch(N, h, x0, up, tr, w, hessian=oracle.HESS_EXACT)
+    assert (r1["status"] == 0).all()
+    rng = np.random.default_rng(5)
+    x0p = x0 + rng.uniform(-1e-7, 1e-7, x0.shape)
+    Vw = r1["V"].copy()
+    Vw[:, :4] = x0p
+    one = oracle.solve_batch(N, h, x0p, up, tr, w, V=Vw, max_iter=1, hessian=oracle.HESS_EXACT)
+    for b in range(len(x0)):
+        _, c0 = oracle.nlp_eval(N, h, Vw[b], up[b], tr[b], w)
+        _, c1 = oracle.nlp_eval(N, h, one["V"][b], up[b], tr[b], w)
+        assert np.abs(c0).sum() <= 1e-4           # nearly feasible: theta_0 <= theta_min
+        assert np.abs(c1).sum() <= np.abs(c0).sum()
+    full = oracle.solve_batch(N, h, x0p, up, tr, w, V=Vw, hessian=oracle.HESS_EXACT)
+    assert (full["status"] == 0).all() and full["iters"].max() <= 3
+
+
+@pytest.mark.parametrize("model,hess", [("two_link", "gn"), ("two_link", "exact"), ("exo", "gn")])
+def test_riccati_restatement_equals_dense(model, hess, oracle):
+    """ORACLE_KKT_RICCATI (the kernels' Riccati recursion on s_k = [dx_k; du_{k-1}], the CPU baseline's
+    same-algorithm leg) solves the same QP as the dense condensed Cholesky: identical iteration counts and
+    statuses, V* within 1e-10 relative (same algorithm)."""
+    if model == "exo":
+        N, m, w, B = 50, oracle.EXO, np.array([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4), 48
+    else:
+        N, m, w, B = 30, oracle.TWO_LINK, np.array(WEIGHTS_CFG), 256
+    hs = oracle.HESS_EXACT if hess == "exact" else oracle.HESS_GAUSS_NEWTON
+    x0, up, tr = oracle.synth(20250213, 0, B, N, 0.002, model=m)
+    d = oracle.solve_batch(N, 0.002, x0, up, tr, w, model=m, hessian=hs, init_states=2)
+    r = oracle.solve_batch(N, 0.002, x0, up, tr, w, model=m, hessian=hs, init_states=2, kkt=oracle.KKT_RICCATI)
+    assert (d["status"] == 0).all()
+    np.testing.assert_array_equal(r["status"], d["status"])
+    np.testing.assert_array_equal(r["iters"], d["iters"])
+    rel = np.abs(r["V"] - d["V"]).max(1) / np.abs(d["V"]).max(1)
+    assert rel.max() <= 1e-10, rel.max()

@@ -24,6 +24,7 @@ ap.add_argument("--key")
 ap.add_argument("--batch", type=int)
 ap.add_argument("--horizon", type=int)
 ap.add_argument("--source")
+ap.add_argument("--lib-sha256", help="sha256 of the library the PMC passes loaded (bench.py merges by it)")
 a = ap.parse_args()
 
 vals = defaultdict(list)
@@ -34,7 +35,7 @@ for f in glob.glob(os.path.join(a.out, "*", "**", "*counter_collection.csv"), re
         vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
 # rocprofv3 csv: one row per (dispatch, counter), already summed over the device
 summary = {k: sum(v) / len(v) for k, v in vals.items()}
-res = {"kernel": a.kernel, "per_dispatch_mean": summary}
+res = {"kernel": a.kernel, "per_dispatch_mean": summary, "lib_sha256": a.lib_sha256}
 durs = []
 for f in glob.glob(os.path.join(a.out, "trace", "**", "*kernel_trace.csv"), recursive=True):
     for row in csv.DictReader(open(f)):
@@ -75,5 +76,6 @@ if a.traffic_json and a.key and "hbm_bytes_per_launch" in res:
                  "lds_bank_conflict_cycles": summary.get("SQ_LDS_BANK_CONFLICT"),
                  "valu_active_frac": (summary["SQ_ACTIVE_INST_VALU"] / summary["SQ_WAVE_CYCLES"]
                                       if summary.get("SQ_WAVE_CYCLES") and "SQ_ACTIVE_INST_VALU" in summary else None),
-                 "source": a.source}
+                 "source": a.source,
+                 "lib_sha256": a.lib_sha256}
     json.dump(tj, open(a.traffic_json, "w"), indent=1)
