@@ -84,6 +84,12 @@ def parse(argv=None):
     ap.add_argument("--no-secondary", action="store_true",
                     help="cfg2 only: skip the cfg#3 / cfg#5 lines the default invocation attaches as 'secondary'")
     ap.add_argument("--no-sweep", action="store_true", help="cfg5: skip the tolerance sweep (single tolerance)")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling: --batch (default: the config's B) is the GLOBAL batch, split over the ranks "
+                         "in contiguous shards (mmpc.dist.shard_strong); default: weak scaling, B per GPU")
+    ap.add_argument("--u-bound", type=float, default=None,
+                    help="control bounds |u| <= U on every instance (update_control_limits, ModelControl.cpp:205-209): "
+                         "the projected GN-SQP (DESIGN.md 3b)")
     ap.add_argument("--init", choices=["zero", "as_given", "hold_x0"], default="zero",
                     help="mmpc_opts.init_states: the reference's cold start V = 0 (zero: MMPC_INIT_ZERO, V not read; "
                          "as_given: V zeroed every step), or x_1..x_N = x_0 (DESIGN 3d)")
@@ -150,7 +156,7 @@ def _cpu_leg(o, cfg, N, h, target_s, kw, kkt):
     return n, time.perf_counter() - t, r
 
 
-def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1):
+def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1, u_bound=None):
     """The oracle (oracle/liboracle.so: the same NLP and SQP in plain C + OpenMP, cold start V = 0) timed on a
     bounded sample of the same seeded workload, in two legs:
       riccati          the Riccati recursion the GPU kernels run (ORACLE_KKT_RICCATI: same algorithm, same iterates)
@@ -164,10 +170,16 @@ def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, he
     # the same SQP as the GPU: the Hessian the library resolved (mmpc_resolve_hessian: 1 Gauss-Newton, 2 exact)
     kw = dict(nthreads=threads, model=model, tol_grad=tol_grad, tol_defect=tol_defect, init_states=2,
               hessian=o.HESS_EXACT if hessian == 2 else o.HESS_GAUSS_NEWTON)
+    nu = cfg["nu"]
+    if u_bound is not None:   # the oracle's projected GN-SQP (its Riccati restatement covers unbounded solves only)
+        kw.update(u_lb=np.full(nu, -u_bound), u_ub=np.full(nu, u_bound))
     hist = lambda a: {int(k): int(v) for k, v in zip(*np.unique(a, return_counts=True))}  # noqa: E731
     legs = {}
-    for name, kkt, what in (("riccati", o.KKT_RICCATI, "Riccati recursion on [dx_k; du_{k-1}] (the GPU's algorithm)"),
-                            ("dense_condensed", o.KKT_DENSE, "DENSE condensed KKT (Cholesky of the N*nu Hessian)")):
+    legs_spec = [("riccati", o.KKT_RICCATI, "Riccati recursion on [dx_k; du_{k-1}] (the GPU's algorithm)"),
+                 ("dense_condensed", o.KKT_DENSE, "DENSE condensed KKT (Cholesky of the N*nu Hessian)")]
+    if u_bound is not None:   # bounded: the oracle's projected GN-SQP exists in the dense form only
+        legs_spec = legs_spec[1:]
+    for name, kkt, what in legs_spec:
         n, dt, r = _cpu_leg(o, cfg, N, h, target_s, kw, kkt)
         m = min(n, gpu_V.shape[0])
         ref = r["V"][:m]
@@ -183,11 +195,10 @@ def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, he
                         max_rel_diff_V_same_iters=float(rel[same_it].max()) if same_it.any() else None,
                         same_iteration_count=int(same_it.sum())),
             iters_hist_cpu=hist(r["iters"]))
-    ric = legs["riccati"]
+    ric = legs.get("riccati") or legs["dense_condensed"]
     return dict(value=ric["value"], unit="solves/s", cores=threads, kind="port",
-                sample=ric["sample"] + " (the dense-condensed leg is reported beside it)",
-                vs_gpu=ric["vs_gpu"], iters_hist_cpu=ric["iters_hist_cpu"], iters_hist_gpu=hist(gpu_iters),
-                riccati=ric, dense_condensed=legs["dense_condensed"])
+                sample=ric["sample"] + (" (the dense-condensed leg is reported beside it)" if "riccati" in legs else ""),
+                vs_gpu=ric["vs_gpu"], iters_hist_cpu=ric["iters_hist_cpu"], iters_hist_gpu=hist(gpu_iters), **legs)
 
 
 def lib_sha256(path: str) -> str:
@@ -216,7 +227,7 @@ class _StandInSolver:
         up.zero_()
         tr.zero_()
 
-    def solve_batch(self, B, x0, up, tr, w, V, st, it, kkt, stream=None):
+    def solve_batch(self, B, x0, up, tr, w, V, st, it, kkt, stream=None, u_lb=None, u_ub=None):
         V.zero_()
         V[:, self.nx:self.nx + self.nu] = x0[:, :self.nu]
         st.zero_()
@@ -259,6 +270,13 @@ def run_config(args, name, world, rank, primary=True):
     cfg = CONFIGS[name]
     B = (args.batch if primary else None) or cfg["B"]
     N = (args.horizon if primary else None) or cfg["N"]
+    # rows of this rank: weak scaling -- B per rank, global instances [r B, (r+1) B); strong -- the global batch B split
+    # in contiguous shards; Bc = result-table rows per rank (equal for the gather; strong shards may be ragged)
+    strong = args.strong and primary
+    Bt = B if strong else B * world
+    Bc = -(-B // world) if strong else B
+    first, n = mdist.shard_strong(B, rank, world) if strong else mdist.shard(B, rank)
+    nrows = [mdist.shard_strong(B, r, world)[1] for r in range(world)] if strong else [B] * world
     nx, nu, h_us = cfg["nx"], cfg["nu"], 2000
     h = h_us * 1e-6
     tol_grad = 1e-8 if args.tol is None else args.tol
@@ -286,17 +304,21 @@ def run_config(args, name, world, rank, primary=True):
                                           "hold_x0": mmpc.INIT_HOLD_X0}[args.init],
                              hessian={"auto": mmpc.HESSIAN_AUTO, "gauss_newton": mmpc.HESSIAN_GAUSS_NEWTON,
                                       "exact": mmpc.HESSIAN_EXACT}[args.hessian if primary else "auto"])
-        solver.reserve_workspace(B)
-        ksolver = solver.kkt_solver_for(B)   # the AUTO choice, resolved by the library
-        hess = solver.hessian_for(B)
+        solver.reserve_workspace(n)
+        ksolver = solver.kkt_solver_for(n)   # the AUTO choice, resolved by the library
+        hess = solver.hessian_for(n, bool(args.u_bound is not None and primary))
         stream = torch.cuda.current_stream(dev)
     NV = solver.NV
     f64 = dict(dtype=torch.float64, device=dev)
-    x0 = torch.empty((B, nx), **f64)
-    up = torch.empty((B, nu), **f64)
-    tr = torch.empty((B, N, nx), **f64)
+    x0 = torch.empty((n, nx), **f64)
+    up = torch.empty((n, nu), **f64)
+    tr = torch.empty((n, N, nx), **f64)
     w = torch.tensor(cfg["weights"], **f64)
-    V = torch.zeros((B, NV), **f64)
+    ulb = uub = None
+    if args.u_bound is not None and primary:
+        ulb = torch.full((nu,), -args.u_bound, **f64)
+        uub = torch.full((nu,), args.u_bound, **f64)
+    V = torch.zeros((n, NV), **f64)
     # results the reference consumes per tick: u_0* (ModelControl.cpp:174-190), status, iterations -- one byte
     # buffer per rank, [B][nu] f64 u_0* | [B] i32 status | [B] i32 iterations.
     # Every step: the solve kernel stores them straight into pinned host memory of the rank's own process
@@ -305,20 +327,20 @@ def run_config(args, name, world, rank, primary=True):
     # N > 1, last step (and last warm-up step): the rank-0 table instead -- the solve writes status and iterations
     #   into a device buffer, u_0* is one strided copy out of V, one all_gather_into_tensor (RCCL over xGMI) to
     #   rank 0's device, then one D2H there; rank 0 checks it against every rank's own results.
-    nbytes = B * (8 * nu + 8)
+    nbytes = Bc * (8 * nu + 8)
     zero_copy = not standin
     hbuf = None
     if zero_copy:
         hbuf = [mmpc.HostBuffer(nbytes) for _ in range(2)]
-        hviews = [(hb.view(0, np.float64, B * nu), hb.view(B * nu * 8, np.int32, B),
-                   hb.view(B * nu * 8 + 4 * B, np.int32, B)) for hb in hbuf]
+        hviews = [(hb.view(0, np.float64, Bc * nu), hb.view(Bc * nu * 8, np.int32, Bc),
+                   hb.view(Bc * nu * 8 + 4 * Bc, np.int32, Bc)) for hb in hbuf]
     res = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-    u0 = res[:B * nu * 8].view(torch.float64).view(B, nu)
-    st = res[B * nu * 8:B * nu * 8 + 4 * B].view(torch.int32)
-    it = res[B * nu * 8 + 4 * B:].view(torch.int32)
+    res.zero_()
+    u0 = res[:Bc * nu * 8].view(torch.float64).view(Bc, nu)
+    st = res[Bc * nu * 8:Bc * nu * 8 + 4 * Bc].view(torch.int32)
+    it = res[Bc * nu * 8 + 4 * Bc:].view(torch.int32)
     sh = stream.cuda_stream if stream is not None else None
-    first, _ = mdist.shard(B, rank)
-    solver.synth(SEED, first, B, x0, up, tr, stream=sh)
+    solver.synth(SEED, first, n, x0, up, tr, stream=sh)
     mdist.broadcast_shared(w)   # shared weights from rank 0 (identical here by construction)
 
     table = torch.empty(world * nbytes, dtype=torch.uint8, device=dev) if world > 1 else res
@@ -333,7 +355,7 @@ def run_config(args, name, world, rank, primary=True):
     def results_to_host(k, last):
         if zc(k, last):
             return   # stored into host memory by the solve kernel
-        u0.copy_(V[:, nx:nx + nu])
+        u0[:n].copy_(V[:, nx:nx + nu])
         if world > 1:   # N > 1: one all_gather_into_tensor (RCCL over xGMI) to rank 0's device, then D2H there
             dist.all_gather_into_tensor(table, res, async_op=True).wait()   # stream-ordered on GPUs
         if rank == 0:
@@ -342,9 +364,9 @@ def run_config(args, name, world, rank, primary=True):
     def launch(k, last):
         if zc(k, last):
             u0h, sth, ith = hviews[k % 2]
-            solver.solve_batch(B, x0, up, tr, w, V, sth, ith, None, stream=sh, u0=u0h)
+            solver.solve_batch(n, x0, up, tr, w, V, sth, ith, None, stream=sh, u0=u0h, u_lb=ulb, u_ub=uub)
         else:
-            solver.solve_batch(B, x0, up, tr, w, V, st, it, None, stream=sh)
+            solver.solve_batch(n, x0, up, tr, w, V, st, it, None, stream=sh, u_lb=ulb, u_ub=uub)
 
     def solve(k, last):
         if zero_v:
@@ -389,18 +411,18 @@ def run_config(args, name, world, rank, primary=True):
         hb = hviews[(args.steps - 1) % 2]
         res.copy_(hbytes(args.steps - 1))
         host[(args.steps - 1) % 2].copy_(res.cpu())
-        zc_ok = bool(np.array_equal(hb[0].reshape(B, nu), V[:, nx:nx + nu].cpu().numpy()))
+        zc_ok = bool(np.array_equal(hb[0][:n * nu].reshape(n, nu), V[:, nx:nx + nu].cpu().numpy()))
     elif zero_copy and args.steps >= 2:   # N > 1: the previous step (same instances) stored into host memory
         zc_ok = bool(torch.equal(hbytes(args.steps - 2), res.cpu()))
-    iters = it.cpu().numpy()
+    iters = it.cpu().numpy()[:n]
     # rank 0's host table of the last step against every rank's own results
     mine = res.cpu()
     ok = zc_ok is not False
     if rank == 0:
         last = host[(args.steps - 1) % 2]
         ok = bool(torch.equal(last[:nbytes], mine)) and ok
-        conv = sum(int((last[r * nbytes + B * nu * 8:r * nbytes + B * nu * 8 + 4 * B].view(torch.int32) == 0).sum())
-                   for r in range(world))
+        conv = sum(int((last[r * nbytes + Bc * nu * 8:r * nbytes + Bc * nu * 8 + 4 * Bc].view(torch.int32)[:nrows[r]]
+                        == 0).sum()) for r in range(world))
         tail = last
     else:
         conv = 0
@@ -408,7 +430,7 @@ def run_config(args, name, world, rank, primary=True):
     if world > 1:
         ok = bool(torch.equal(table[rank * nbytes:(rank + 1) * nbytes].cpu(), mine)) and ok
         ok = mdist.sum_over_ranks(int(not ok), device=dev if not standin else None) == 0
-    total = B * world * args.steps
+    total = Bt * args.steps
     value = total / elapsed
     out = {
         "metric": cfg["metric"],
@@ -419,12 +441,14 @@ def run_config(args, name, world, rank, primary=True):
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64" if not cfg["fp32"] else "f64 (fp32 Riccati factor)",
         "data": f"synthetic: counter-based splitmix64 {name} instances (SURVEY.md 8d), generated on device "
                 f"from (seed, global instance index), so N = 1 and N > 1 solve identical instances",
-        "config": {"workload": cfg["workload"], "batch_per_gpu": B, "global_batch": B * world,
+        "config": {"workload": cfg["workload"] + (f"; control bounds |u| <= {args.u_bound} (projected GN-SQP)"
+                                                  if ulb is not None else ""),
+                   "batch_per_gpu": n, "global_batch": Bt,
                    "horizon": N, "tol_grad": tol_grad, "tol_defect": tol_defect,
                    "kkt_solver": {0: "stand-in (test)", 1: "condensed (wave per instance)",
                                   2: "riccati (lane per instance)", 3: "riccati (16 lanes per instance)"}[ksolver],
@@ -451,16 +475,16 @@ def run_config(args, name, world, rank, primary=True):
         out["standin"] = True
         if tail is not None:   # u_0*[:, 0] of every rank's slice of the gathered table
             out["standin_u0_first_col"] = [v for r in range(world)
-                                           for v in tail[r * nbytes:r * nbytes + B * nu * 8].view(torch.float64)
-                                           .view(B, nu)[:, 0].tolist()]
+                                           for v in tail[r * nbytes:r * nbytes + Bc * nu * 8].view(torch.float64)
+                                           .view(Bc, nu)[:nrows[r], 0].tolist()]
     else:
         out["kernel_ms"] = kern_ms
-        out["roofline"] = roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms)
+        out["roofline"] = roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, n, iters, kern_ms, hess)
     if name == "cfg5" and world == 1 and not standin and not args.no_sweep:
-        out["tolerance_sweep"] = cfg5_sweep(path, cfg, B, x0, up, tr, w, args.hessian)
+        out["tolerance_sweep"] = cfg5_sweep(path, cfg, n, x0, up, tr, w, args.hessian)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin and name != "cfg5":
         out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
-                                           tol_defect, hess)
+                                           tol_defect, hess, None if ulb is None else args.u_bound)
     if hbuf:
         for hb in hbuf:
             hb.close()
@@ -509,7 +533,7 @@ def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3):
     return rows
 
 
-def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms):
+def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms, hess):
     """FP64-VALU roofline of the solve kernel (the only kernel of a step besides a memset and the result pack).
 
     achieved = the kernel's OWN algorithmic flop count (mmpc.*_flops_per_iteration: structure-exploiting, no
@@ -520,7 +544,7 @@ def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_m
     algorithm-equivalent rate: it is NOT the work the kernel does."""
     riccati = ksolver in (2, 3)
     if riccati:
-        fl = mmpc.riccati_flops_per_iteration(N, nx, nu, exact=solver.hessian_for(B) == mmpc.HESSIAN_EXACT)
+        fl = mmpc.riccati_flops_per_iteration(N, nx, nu, exact=hess == mmpc.HESSIAN_EXACT)
         model = "ExoArm" if cfg["model"] == "exo_arm" else "TwoLinkArm"
         if ksolver == 3:
             kname = f"sqp_group_kernel<{model}"

@@ -633,12 +633,14 @@ int resolve_hessian(const mmpc_handle* h, int solver, bool u_bounded) {
         dflt = ExactDefault<M>::value;
         return MMPC_OK;
     });
-    const bool ok = capable && solver == MMPC_KKT_RICCATI_GROUP && !u_bounded && !h->x_bounded &&
-                    !h->info.is_linear && !h->opts.factor_fp32;
+    // control bounds (the projected SQP): held controls are fixed in the exact QP as in the Gauss-Newton one
+    (void)u_bounded;
+    const bool ok = capable && solver == MMPC_KKT_RICCATI_GROUP && !h->x_bounded && !h->info.is_linear &&
+                    !h->opts.factor_fp32;
     if (want == MMPC_HESSIAN_EXACT) {
         if (!ok)
             return fail(MMPC_ERR_UNSUPPORTED, "exact Hessian: needs a model with second derivatives, the "
-                                              "RICCATI_GROUP solver and an unbounded nonlinear solve");
+                                              "RICCATI_GROUP solver and a nonlinear solve without state bounds");
         return MMPC_HESSIAN_EXACT;
     }
     return ok && dflt ? MMPC_HESSIAN_EXACT : MMPC_HESSIAN_GAUSS_NEWTON;
@@ -753,7 +755,9 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
             if constexpr (exact_capable<M>()) {
-                if (hess == MMPC_HESSIAN_EXACT) return launch_group<M, false, false, true>(grid, block, lds, stream, p, gwk);
+                if (hess == MMPC_HESSIAN_EXACT)
+                    return bounded ? launch_group<M, true, false, true>(grid, block, lds, stream, p, gwk)
+                                   : launch_group<M, false, false, true>(grid, block, lds, stream, p, gwk);
             }
             if (xb) return launch_group<M, false, true>(grid, block, lds, stream, p, gwk);
             return bounded ? launch_group<M, true>(grid, block, lds, stream, p, gwk)
@@ -1341,6 +1345,15 @@ int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) {
         unsigned long long z[16] = {0};
         MMPC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z)));
     }
+    return MMPC_OK;
+}
+
+// Internal diagnostic (not part of include/mmpc.h): the handle's Riccati workspace (device pointer and size), e.g. to
+// read the gains [K_k | kff_k] a solve left there (tools/xb_diag.py)
+int mmpc_debug_workspace(mmpc_handle* h, void** ptr, uint64_t* bytes) {
+    if (!h || !ptr || !bytes) return fail(MMPC_ERR_INVALID_ARG, "null argument");
+    *ptr = h->ws;
+    *bytes = h->ws_bytes;
     return MMPC_OK;
 }
 

@@ -191,9 +191,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     load_bounds<NU, BOUNDED>(p, lbv, ubv);
     // ---- lane-distributed Riccati (DIST): lane r of the group owns row r of the augmented value function
     //      P~ (NS x NS) and of every per-row quantity; small per-stage quantities are computed redundantly on
-    //      all lanes; rows are exchanged with row_bcast.  Bounded / state-bounded solves keep
-    //      the one-lane sweep below. ----
-    constexpr bool DIST = (NS < G) && !BOUNDED && !XB;
+    //      all lanes; rows are exchanged with row_bcast.  Control bounds (BOUNDED) run the same
+    //      sweeps with the held controls of the projected GN-SQP folded into the per-stage quantities; state-bounded
+    //      solves keep the one-lane sweep below. ----
+    constexpr bool DIST = (NS < G) && !XB;
     static_assert(!EXACT || (DIST && HasHess<Model>::value), "exact Hessian: lane-distributed path, model eval_hess");
     const int r = gl;
     const bool lx = r < NX, lu = r >= NX && r < NS, la = r >= NQ && r < NX;
@@ -209,6 +210,13 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     const double lxf = lx ? 1.0 : 0.0;
     const int rq = r < NQ ? r : 0;                    // q column of a q-lane (clamped)
     const double Rr = lu ? w[NX + ru] : 0.0;          // R of this lane's u row
+    double lbr = -INFINITY, ubr = INFINITY;            // bounds of this u-lane's control (BOUNDED)
+#pragma unroll
+    for (int c = 0; c < NU; ++c)
+        if (lu && ru == c) {
+            lbr = lbv[c];
+            ubr = ubv[c];
+        }
     double hq[NQ > 0 ? NQ : 1], hrow[NX], qoh[NX], rdg[NU];
 #pragma unroll
     for (int z = 0; z < NQ; ++z) hq[z] = (r == NQ + z) ? h : 0.0;   // column r of A holds h in row z (kinematics)
@@ -857,7 +865,14 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     const double uk = sU[k * NU + c], um = k == 0 ? up[c] : sU[(k - 1) * NU + c];
                     g = fma(R[c], uk - um, fma(Rm[c], uk, g));
                     if (k < N - 1) g -= R[c] * (sU[(k + 1) * NU + c] - uk);
-                    gmax = fmax(gmax, fabs(2.0 * g));
+                    if constexpr (!BOUNDED) {
+                        gmax = fmax(gmax, fabs(2.0 * g));
+                    } else {   // projected gradient; epsilon-active holds of the first QP solve (oracle solve_one)
+                        gmax = fmax(gmax, fabs(uk - proj(uk - 2.0 * g, lbv[c], ubv[c])));
+                        sHold[k * NU + c] = (uk <= lbv[c] + beps && g > 0.0)   ? lbv[c]
+                                            : (uk >= ubv[c] - beps && g < 0.0) ? ubv[c]
+                                                                                : NAN;
+                    }
                     nonfinite |= !isfinite(g);
                 }
             }
@@ -964,6 +979,42 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     Ycol[a] = colA(T[a], acol, tb) - rdg[a];
                     if constexpr (EXACT) Ycol[a] += wr[NX + a];   // H_wx[a][r] += W_ux[a][r] (x-lanes; 0 else)
                 }
+                // held controls (BOUNDED, sHold of this QP solve): du_a = target - u_a fixed in the stage QP, as the
+                // one-lane sweep -- p~ gains [H_wx | -R]^T delta, h_w the coupling H_ww delta, the held rows and
+                // columns of H_ww become the identity and the held rows of [H_wx | -R] zero, so that K_a = 0 and
+                // kff_a = delta_a exactly; Rk: the -R columns of the u-lanes with the held rows removed
+                double pexr = 0.0, Rk[NU];
+#pragma unroll
+                for (int c = 0; c < NU; ++c) Rk[c] = R[c];
+                if constexpr (BOUNDED) {
+                    bool hd[NU];
+                    double dl[NU], hw2[NU];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        const double tg = sHold[k * NU + a];
+                        hd[a] = tg == tg;
+                        dl[a] = hd[a] ? tg - u[a] : 0.0;
+                        pexr = fma(Ycol[a], dl[a], pexr);
+                    }
+#pragma unroll
+                    for (int b = 0; b < NU; ++b) {
+                        double t = hw[b];
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) t = fma(Hww[a][b], dl[a], t);
+                        hw2[b] = hd[b] ? -dl[b] : t;
+                    }
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        hw[a] = hw2[a];
+#pragma unroll
+                        for (int b = 0; b < NU; ++b)
+                            if (hd[a] || hd[b]) Hww[a][b] = (a == b) ? 1.0 : 0.0;
+                        if (hd[a]) {
+                            Ycol[a] = 0.0;
+                            Rk[a] = 0.0;
+                        }
+                    }
+                }
                 // Kcol = H_ww^-1 Ycol (this lane's column of K~), kff = H_ww^-1 h_w (redundant)
                 double Kcol[NU], kff[NU], Ku[NU][NU];
                 if constexpr (NU == 2) {
@@ -975,10 +1026,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     Kcol[1] = fma(i01, Ycol[0], i11 * Ycol[1]);
                     kff[0] = fma(i00, hw[0], i01 * hw[1]);
                     kff[1] = fma(i01, hw[0], i11 * hw[1]);
-                    Ku[0][0] = -i00 * R[0];
-                    Ku[0][1] = -i01 * R[1];
-                    Ku[1][0] = -i01 * R[0];
-                    Ku[1][1] = -i11 * R[1];
+                    Ku[0][0] = -i00 * Rk[0];
+                    Ku[0][1] = -i01 * Rk[1];
+                    Ku[1][0] = -i01 * Rk[0];
+                    Ku[1][1] = -i11 * Rk[1];
                 } else {   // Cholesky H_ww = L L^T (rsq + Newton), solves with L and L^T
                     double Ld[NU][NU], il[NU];
 #pragma unroll
@@ -1024,7 +1075,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     for (int c = 0; c < NU; ++c) {   // column NX + c of K~: H_ww^-1 (-R_c e_c)
                         double e[NU], o[NU];
 #pragma unroll
-                        for (int a = 0; a < NU; ++a) e[a] = (a == c) ? -R[c] : 0.0;
+                        for (int a = 0; a < NU; ++a) e[a] = (a == c) ? -Rk[c] : 0.0;
                         chol_solve(e, o);
 #pragma unroll
                         for (int a = 0; a < NU; ++a) Ku[a][c] = o[a];
@@ -1080,6 +1131,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 double pv2 = pn;
 #pragma unroll
                 for (int a = 0; a < NU; ++a) pv2 = fma(-Ycol[a], kff[a], pv2);
+                if constexpr (BOUNDED) pv2 += pexr;
                 pvr = pv2;
             };
             // inner stages N-1 .. 1 by unconditional pairs (an odd count peels stage N-1 in front), as the step sweep
@@ -1203,12 +1255,15 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
+        // exact Hessian in this iteration's QP solves (false after a Gauss-Newton fallback)
+        bool use_w = EXACT;
         if constexpr (DIST) {   // Riccati sweep (fact_ok is uniform over the group)
-            backward_dist(EXACT);
+            backward_dist(use_w);
             // exact KKT matrix not positive definite on the null space: this iteration takes the Gauss-Newton step
             // (oracle solve_one: Cholesky of the exact condensed Hessian fails -> Gauss-Newton)
             if (EXACT && !fact_ok) {
                 fact_ok = 1;
+                use_w = false;
                 backward_dist(false);
             }
         }
@@ -1227,7 +1282,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             // step sweep: lane r holds s_k[r], s = [dx_k; du_{k-1}]; u-lanes du_k = K_k s_k + kff_k (row r - NX of
             // K from the workspace), x-lanes dx_{k+1} = A dx + B du + c.  A dx_k + B du_k goes to sD[k+1] (d is
             // dead after the backward sweep) for the directional derivative below.
-            if (fact_ok) {
+            // check: a free control whose step crosses a bound is held there (sHold) and the QP solved again (BOUNDED)
+            auto step_dist = [&](bool check) {
                 // K_k columns were stored by the other lanes of this wave in the backward sweep
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -1269,6 +1325,15 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         sD[(k + 1) * NX + rx] = ad;
                     }
                     if (lu) sDU[k * NU + ru] = du;
+                    if constexpr (BOUNDED) {
+                        if (check && lu) {
+                            const double hv = sHold[k * NU + ru], t = sU[k * NU + ru] + du;
+                            if (hv != hv && (t < lbr || t > ubr)) {
+                                sHold[k * NU + ru] = t < lbr ? lbr : ubr;
+                                resolve = true;
+                            }
+                        }
+                    }
                     sr = lx ? dxn : (lu ? du : 0.0);
                     fetch(k + 3 < N ? k + 3 : N - 1, o);   // unconditional: static wait counts
                 };
@@ -1303,6 +1368,27 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         stage(k + 1, o1);
                         stage(k + 2, o2);
                     }
+                }
+            };
+            for (int pass = 0;; ++pass) {
+                if (pass > 0) {   // BOUNDED: controls held after the previous step -- solve the QP again
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                    backward_dist(use_w);
+                    if (EXACT && use_w && !fact_ok) {   // the held exact QP not positive definite: Gauss-Newton
+                        fact_ok = 1;
+                        use_w = false;
+                        backward_dist(false);
+                    }
+                    if (!fact_ok) break;
+                }
+                resolve = false;
+                step_dist(BOUNDED && pass + 1 < kBoundPasses);
+                if constexpr (!BOUNDED) {
+                    break;
+                } else {
+                    resolve = group_max(resolve ? 1.0 : 0.0) != 0.0;
+                    if (!resolve || pass + 1 >= kBoundPasses) break;
                 }
             }
             __builtin_amdgcn_wave_barrier();

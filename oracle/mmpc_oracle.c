@@ -304,6 +304,9 @@ static int model_hess(const double* x, const double* u, const double* lam, doubl
 /* mmpc_opts.hessian (process-wide): ORACLE_HESS_GAUSS_NEWTON or ORACLE_HESS_EXACT */
 static int g_hess_mode = ORACLE_HESS_GAUSS_NEWTON;
 void oracle_set_hessian(int mode) { g_hess_mode = mode; }
+/* EXACT with control bounds: the held controls fixed in the exact QP (1), or such solves keep Gauss-Newton (0) */
+static int g_exact_bounded = 1;
+void oracle_set_exact_bounded(int on) { g_exact_bounded = on; }
 
 void oracle_two_link_xdot(const double* x, const double* u, double* xdot) {
     oracle_two_link_jac(x, u, NULL, NULL, xdot);
@@ -453,6 +456,7 @@ typedef struct {
     int N, M;
     double *X, *U, *F, *Ad, *Bd, *c, *d, *e, *G, *H, *g, *du, *dx, *lam, *Xt, *Ut, *Ft, *H0, *g0, *tgt;
     double *Kf, *Wk;  /* Riccati variant: [K_k | kff_k] per stage, exact-Hessian stage blocks W_k */
+    double *Hgn, *ggn; /* exact Hessian: the Gauss-Newton QP of the same iteration (fallback when not PD) */
 } ws_t;
 
 static void ws_alloc(ws_t* s, int N) {
@@ -480,12 +484,14 @@ static void ws_alloc(ws_t* s, int N) {
     s->tgt = calloc(M, sizeof(double));
     s->Kf = calloc((size_t)N * NU * (NX + NU + 1), sizeof(double));
     s->Wk = calloc((size_t)N * (NX + NU) * (NX + NU), sizeof(double));
+    s->Hgn = calloc(M * M, sizeof(double));
+    s->ggn = calloc(M, sizeof(double));
 }
 static void ws_free(ws_t* s) {
     free(s->X); free(s->U); free(s->F); free(s->Ad); free(s->Bd); free(s->c); free(s->d);
     free(s->e); free(s->G); free(s->H); free(s->g); free(s->du); free(s->dx); free(s->lam);
     free(s->Xt); free(s->Ut); free(s->Ft); free(s->H0); free(s->g0); free(s->tgt);
-    free(s->Kf); free(s->Wk);
+    free(s->Kf); free(s->Wk); free(s->Hgn); free(s->ggn);
 }
 
 /* merit pieces at (X,U): J and sum |c| (F returned) */
@@ -690,15 +696,16 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
          * whose step leaves the box is then held at the bound it crosses and the QP solved again (at most
          * ORACLE_BOUND_PASSES solves; the projected line search absorbs what is left). */
         int fact_fail = 0;
-        if (has_b) { memcpy(s->H0, s->H, sizeof(double) * M * M); memcpy(s->g0, s->g, sizeof(double) * M); }
         /* exact Hessian (ORACLE_HESS_EXACT): the QP in (dx, du) gains the stage term 1/2 [dx_k; du_k]^T W_k [..]
          * with W_k = h sum_r lam_{k+1,r} d^2 f_r/d(x_k,u_k)^2 (J/2 scale, lam of step 5); condensed with
          * dx_k = Gamma_k du + d_k (S_k du = [Gamma_k du; du_k]):  H += S_k^T W_k S_k,  g += S_k^T W_k [d_k; 0].
-         * The stop test above used the true reduced gradient; W only changes the step. */
-        const int use_exact = g_hess_mode == ORACLE_HESS_EXACT && !has_b && !g_lin && model_has_hess();
+         * The stop test above used the true reduced gradient; W only changes the step.  With control bounds the
+         * held controls are fixed in this exact QP as in the Gauss-Newton one (g_exact_bounded). */
+        const int use_exact = g_hess_mode == ORACLE_HESS_EXACT && (!has_b || g_exact_bounded) && !g_lin &&
+                              model_has_hess();
         if (use_exact) {
-            memcpy(s->H0, s->H, sizeof(double) * M * M);
-            memcpy(s->g0, s->g, sizeof(double) * M);
+            memcpy(s->Hgn, s->H, sizeof(double) * M * M);
+            memcpy(s->ggn, s->g, sizeof(double) * M);
             const int K = NX + NU;
             double W[(ORACLE_MAX_NX + ORACLE_MAX_NU) * (ORACLE_MAX_NX + ORACLE_MAX_NU)];
             double* T = s->G;  /* Gamma is read below only through S; W S goes to a scratch row block */
@@ -730,6 +737,8 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
             }
             free(WS);
         }
+        if (has_b) { memcpy(s->H0, s->H, sizeof(double) * M * M); memcpy(s->g0, s->g, sizeof(double) * M); }
+        int gn_fallback = 0;
         for (int pass = 0;; ++pass) {
             if (has_b) {
                 if (pass) memcpy(s->H, s->H0, sizeof(double) * M * M);
@@ -747,10 +756,18 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
             }
             for (int a = 0; a < M; ++a) s->du[a] = -s->g[a];
             if (chol_solve(M, s->H, s->du) != 0) {
-                if (!use_exact) { fact_fail = 1; break; }
+                if (!use_exact || gn_fallback) { fact_fail = 1; break; }
                 /* exact KKT matrix not positive definite: this iteration takes the Gauss-Newton step */
-                memcpy(s->H, s->H0, sizeof(double) * M * M);
-                for (int a = 0; a < M; ++a) s->du[a] = -s->g0[a];
+                gn_fallback = 1;
+                if (has_b) {   /* the same pass again on the Gauss-Newton QP */
+                    memcpy(s->H0, s->Hgn, sizeof(double) * M * M);
+                    memcpy(s->g0, s->ggn, sizeof(double) * M);
+                    memcpy(s->H, s->Hgn, sizeof(double) * M * M);
+                    --pass;
+                    continue;
+                }
+                memcpy(s->H, s->Hgn, sizeof(double) * M * M);
+                for (int a = 0; a < M; ++a) s->du[a] = -s->ggn[a];
                 if (chol_solve(M, s->H, s->du) != 0) { fact_fail = 1; break; }
             }
             if (!has_b || pass + 1 >= ORACLE_BOUND_PASSES) break;

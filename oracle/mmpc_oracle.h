@@ -45,6 +45,9 @@ int oracle_set_user_model_hess(oracle_user_hess_fn hess);
  * exact KKT matrix is not positive definite on the null space falls back to Gauss-Newton. */
 enum { ORACLE_HESS_GAUSS_NEWTON = 0, ORACLE_HESS_EXACT = 1 };
 void oracle_set_hessian(int mode);
+/* EXACT with control bounds (projected SQP): 1 (default) = the held controls are fixed in the exact QP as in the
+ * Gauss-Newton one (the kernels' bounded exact-Hessian path); 0 = bounded solves keep the Gauss-Newton Hessian */
+void oracle_set_exact_bounded(int on);
 /* W = sum_r lam[r] d^2 f_r/d(x,u)^2 of the 2-link arm (6x6 row-major, x then u; lam[4]) */
 void oracle_two_link_hess(const double* x, const double* u, const double* lam, double* W);
 

@@ -6,6 +6,7 @@ import json
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 
@@ -131,14 +132,17 @@ def test_auto_solver_policy(tmp_path, model_json, mmpc_mod):
 
 
 def test_hessian_policy(tmp_path, model_json, mmpc_mod):
-    """mmpc_opts.hessian (include/mmpc.h) resolved without a GPU: AUTO = exact for unbounded nonlinear 2-link solves
-    on the group kernel, Gauss-Newton for bounded / linear / exo / lane-kernel solves; EXACT where unsupported is
-    an API error."""
+    """mmpc_opts.hessian (include/mmpc.h) resolved without a GPU: AUTO = exact for nonlinear 2-link solves on the
+    group kernel, with or without control bounds (the held controls are fixed in the exact QP, DESIGN.md 3b);
+    Gauss-Newton for state-bounded / linear / exo / lane-kernel solves; EXACT where unsupported is an API error."""
     m = mmpc_mod
     s = m.Solver(model_json(N=30))
     assert s.hessian_for(4096) == m.HESSIAN_EXACT and s.hessian_for(64) == m.HESSIAN_EXACT
-    assert s.hessian_for(4096, u_bounded=True) == m.HESSIAN_GAUSS_NEWTON
+    assert s.hessian_for(4096, u_bounded=True) == m.HESSIAN_EXACT
     assert s.hessian_for(65536) == m.HESSIAN_GAUSS_NEWTON                 # lane kernel
+    s.set_state_bounds([-np.inf, -np.inf, -1.5, -1.5], [np.inf, np.inf, 1.5, 1.5])
+    assert s.hessian_for(4096) == m.HESSIAN_GAUSS_NEWTON                  # state bounds: interior point, GN
+    s.set_state_bounds(None, None)
     assert m.Solver(model_json(N=30, name="lin", is_linear=True)).hessian_for(64) == m.HESSIAN_GAUSS_NEWTON
     assert m.Solver(model_json(N=30, name="gn"), hessian=m.HESSIAN_GAUSS_NEWTON).hessian_for(4096) == 1
     p = m.write_model_json(str(tmp_path / "exo20.json"), "exo20", 8, 4, 2000, 20, model="exo_arm")
@@ -149,9 +153,10 @@ def test_hessian_policy(tmp_path, model_json, mmpc_mod):
     with pytest.raises(m.MmpcError):
         m.Solver(model_json(N=30, name="bad"), hessian=7)
     s = m.Solver(model_json(N=30, name="ex"), hessian=m.HESSIAN_EXACT)
-    assert s.hessian_for(4096) == m.HESSIAN_EXACT
+    assert s.hessian_for(4096) == m.HESSIAN_EXACT and s.hessian_for(4096, u_bounded=True) == m.HESSIAN_EXACT
+    s.set_state_bounds([-1.0] * 4, [1.0] * 4)
     with pytest.raises(m.MmpcError):
-        s.hessian_for(4096, u_bounded=True)
+        s.hessian_for(4096)
 
 
 def test_invalid_opts_rejected(model_json, mmpc_mod):

@@ -44,3 +44,15 @@ def test_launcher_propagates_rank_failure():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--standin", "--gpus", "2",
                         "--config", "nope"], capture_output=True, text=True, timeout=120, env=env)
     assert p.returncode != 0
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("gpus", [2, 3])
+def test_launcher_strong_scaling_ragged(gpus):
+    """--strong: the global batch (here 10, ragged over 3 ranks) is split in contiguous shard_strong shards; the
+    gathered table holds every global instance once, in order, and value counts the global batch per step."""
+    out = _run("--standin", "--strong", "--gpus", str(gpus), "--batch", "10", "--steps", "3", "--warmup", "1",
+               "--no-cpu-baseline")
+    assert out["scaling"] == "strong" and out["config"]["global_batch"] == 10
+    assert out["gathered_results_match"] is True and out["converged"] == 10
+    assert out["standin_u0_first_col"] == [float(i) for i in range(10)]

@@ -26,6 +26,8 @@ ap.add_argument("--config", choices=["cfg2", "cfg3"], default="cfg2")
 ap.add_argument("--batch", type=int, default=None)
 ap.add_argument("--horizon", type=int, default=None)
 ap.add_argument("--kkt", type=int, default=0, help="kkt_solver (0 auto, 1 condensed, 2 riccati)")
+ap.add_argument("--u-bound", type=float, default=None, help="control bounds |u| <= U (projected SQP)")
+ap.add_argument("--hessian", type=int, default=0, help="mmpc_opts.hessian (0 auto, 1 Gauss-Newton, 2 exact)")
 a = ap.parse_args()
 exo = a.config == "cfg3"
 B = a.batch or (65536 if exo else 4096)
@@ -34,7 +36,7 @@ nx, nu = (8, 4) if exo else (4, 2)
 L = mmpc.lib()
 L.mmpc_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
 path = mmpc.write_model_json("/tmp/mmpc_phase.json", "phase", nx, nu, 2000, N)
-s = mmpc.Solver(path, kkt_solver=a.kkt)
+s = mmpc.Solver(path, kkt_solver=a.kkt, hessian=a.hessian)
 NAMES_GROUP = ["load", "A:evals(parallel)", "B:d+adjoint(+riccati if not DIST)", "riccati(DIST)+mu",
                "C:step(serial)+dJ", "D:line_search", "after_loop", "writeback", "update(loop top)", "check"]
 if a.kkt == 3:
@@ -46,19 +48,21 @@ x0 = torch.empty((B, nx), **f); up = torch.empty((B, nu), **f); tr = torch.empty
 s.synth(20250213, 0, B, x0, up, tr)
 w = torch.tensor([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4 if exo else [10, 1, 5, 5, 5, 5, .01, .01], **f)
 V = torch.zeros((B, s.NV), **f)
+lb = None if a.u_bound is None else torch.full((nu,), -a.u_bound, **f)
+ub = None if a.u_bound is None else torch.full((nu,), a.u_bound, **f)
 it = torch.zeros(B, dtype=torch.int32, device="cuda")
-s.solve_batch(B, x0, up, tr, w, V, None, it, None)
+s.solve_batch(B, x0, up, tr, w, V, None, it, None, u_lb=lb, u_ub=ub)
 torch.cuda.synchronize()
 buf = (C.c_ulonglong * 16)()
 L.mmpc_debug_phase_cycles(buf, 1)
 V.zero_()
-s.solve_batch(B, x0, up, tr, w, V, None, it, None)
+s.solve_batch(B, x0, up, tr, w, V, None, it, None, u_lb=lb, u_ub=ub)
 torch.cuda.synchronize()
 L.mmpc_debug_phase_cycles(buf, 1)
 cyc = np.array(buf[:10], dtype=np.float64)
 waves = buf[15]
 iters = it.cpu().numpy()
-out = {"config": a.config, "waves": int(waves), "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
+out = {"config": a.config, "u_bound": a.u_bound, "hessian": s.hessian_for(B, a.u_bound is not None), "waves": int(waves), "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
        "cycles_per_wave": float(cyc.sum() / waves),
        "per_phase_cycles_per_wave_iteration": {n: float(c / waves / (iters.mean() + 1)) for n, c in zip(NAMES, cyc)},
        "share": {n: float(c / cyc.sum()) for n, c in zip(NAMES, cyc)}}
