@@ -87,6 +87,9 @@ def parse(argv=None):
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: --batch (default: the config's B) is the GLOBAL batch, split over the ranks "
                          "in contiguous shards (mmpc.dist.shard_strong); default: weak scaling, B per GPU")
+    ap.add_argument("--x-bound", type=float, default=None,
+                    help="state bounds |qdot_i| <= X on the velocity half of x (x_min/x_max, ModelControl.cpp:37-50): "
+                         "the primal-dual interior-point variant (DESIGN.md 3c)")
     ap.add_argument("--u-bound", type=float, default=None,
                     help="control bounds |u| <= U on every instance (update_control_limits, ModelControl.cpp:205-209): "
                          "the projected GN-SQP (DESIGN.md 3b)")
@@ -156,7 +159,8 @@ def _cpu_leg(o, cfg, N, h, target_s, kw, kkt):
     return n, time.perf_counter() - t, r
 
 
-def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1, u_bound=None):
+def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1, u_bound=None,
+                 x_bound=None):
     """The oracle (oracle/liboracle.so: the same NLP and SQP in plain C + OpenMP, cold start V = 0) timed on a
     bounded sample of the same seeded workload, in two legs:
       riccati          the Riccati recursion the GPU kernels run (ORACLE_KKT_RICCATI: same algorithm, same iterates)
@@ -173,11 +177,14 @@ def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, he
     nu = cfg["nu"]
     if u_bound is not None:   # the oracle's projected GN-SQP (its Riccati restatement covers unbounded solves only)
         kw.update(u_lb=np.full(nu, -u_bound), u_ub=np.full(nu, u_bound))
+    if x_bound is not None:   # the oracle's interior-point variant (solve_one_ip, dense)
+        half = cfg["nx"] // 2
+        kw.update(x_lb=np.array([-np.inf] * half + [-x_bound] * half), x_ub=np.array([np.inf] * half + [x_bound] * half))
     hist = lambda a: {int(k): int(v) for k, v in zip(*np.unique(a, return_counts=True))}  # noqa: E731
     legs = {}
     legs_spec = [("riccati", o.KKT_RICCATI, "Riccati recursion on [dx_k; du_{k-1}] (the GPU's algorithm)"),
                  ("dense_condensed", o.KKT_DENSE, "DENSE condensed KKT (Cholesky of the N*nu Hessian)")]
-    if u_bound is not None:   # bounded: the oracle's projected GN-SQP exists in the dense form only
+    if u_bound is not None or x_bound is not None:   # bounded: the oracle's bounded solves are dense only
         legs_spec = legs_spec[1:]
     for name, kkt, what in legs_spec:
         n, dt, r = _cpu_leg(o, cfg, N, h, target_s, kw, kkt)
@@ -304,6 +311,9 @@ def run_config(args, name, world, rank, primary=True):
                                           "hold_x0": mmpc.INIT_HOLD_X0}[args.init],
                              hessian={"auto": mmpc.HESSIAN_AUTO, "gauss_newton": mmpc.HESSIAN_GAUSS_NEWTON,
                                       "exact": mmpc.HESSIAN_EXACT}[args.hessian if primary else "auto"])
+        if args.x_bound is not None and primary:
+            half = nx // 2
+            solver.set_state_bounds([-np.inf] * half + [-args.x_bound] * half, [np.inf] * half + [args.x_bound] * half)
         solver.reserve_workspace(n)
         ksolver = solver.kkt_solver_for(n)   # the AUTO choice, resolved by the library
         hess = solver.hessian_for(n, bool(args.u_bound is not None and primary))
@@ -446,8 +456,10 @@ def run_config(args, name, world, rank, primary=True):
         "dtype": "f64" if not cfg["fp32"] else "f64 (fp32 Riccati factor)",
         "data": f"synthetic: counter-based splitmix64 {name} instances (SURVEY.md 8d), generated on device "
                 f"from (seed, global instance index), so N = 1 and N > 1 solve identical instances",
-        "config": {"workload": cfg["workload"] + (f"; control bounds |u| <= {args.u_bound} (projected GN-SQP)"
-                                                  if ulb is not None else ""),
+        "config": {"workload": cfg["workload"] + (f"; control bounds |u| <= {args.u_bound} (projected SQP)"
+                                                  if ulb is not None else "")
+                   + (f"; state bounds |qdot| <= {args.x_bound} (interior point)"
+                      if args.x_bound is not None and primary else ""),
                    "batch_per_gpu": n, "global_batch": Bt,
                    "horizon": N, "tol_grad": tol_grad, "tol_defect": tol_defect,
                    "kkt_solver": {0: "stand-in (test)", 1: "condensed (wave per instance)",
@@ -484,7 +496,8 @@ def run_config(args, name, world, rank, primary=True):
         out["tolerance_sweep"] = cfg5_sweep(path, cfg, n, x0, up, tr, w, args.hessian)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin and name != "cfg5":
         out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
-                                           tol_defect, hess, None if ulb is None else args.u_bound)
+                                           tol_defect, hess, None if ulb is None else args.u_bound,
+                                           args.x_bound if primary else None)
     if hbuf:
         for hb in hbuf:
             hb.close()

@@ -192,9 +192,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     // ---- lane-distributed Riccati (DIST): lane r of the group owns row r of the augmented value function
     //      P~ (NS x NS) and of every per-row quantity; small per-stage quantities are computed redundantly on
     //      all lanes; rows are exchanged with row_bcast.  Control bounds (BOUNDED) run the same
-    //      sweeps with the held controls of the projected GN-SQP folded into the per-stage quantities; state-bounded
-    //      solves keep the one-lane sweep below. ----
-    constexpr bool DIST = (NS < G) && !XB;
+    //      sweeps with the held controls of the projected SQP folded into the per-stage quantities; state bounds
+    //      (XB) add the barrier terms and use the Cholesky (Y^T Y) form of the stage update.  Models with
+    //      nx + nu >= 16 keep the one-lane sweep below. ----
+    constexpr bool DIST = (NS < G);
     static_assert(!EXACT || (DIST && HasHess<Model>::value), "exact Hessian: lane-distributed path, model eval_hess");
     const int r = gl;
     const bool lx = r < NX, lu = r >= NX && r < NS, la = r >= NQ && r < NX;
@@ -210,6 +211,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     const double lxf = lx ? 1.0 : 0.0;
     const int rq = r < NQ ? r : 0;                    // q column of a q-lane (clamped)
     const double Rr = lu ? w[NX + ru] : 0.0;          // R of this lane's u row
+    double dgx[NS];                                    // XB: this x-lane's diagonal entry of P~ (barrier Sigma)
+#pragma unroll
+    for (int j = 0; j < NS; ++j) dgx[j] = (lx && j == r) ? 1.0 : 0.0;
     double lbr = -INFINITY, ubr = INFINITY;            // bounds of this u-lane's control (BOUNDED)
 #pragma unroll
     for (int c = 0; c < NU; ++c)
@@ -815,6 +819,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             {
                 const double eb = lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0;   // x_N - r_{N-1}
                 lamr = Qr * (sD[N * NX + rx] + eb);
+                if constexpr (XB) lamr += lxf * sZg[(N - 1) * NY + rx];   // z_u - z_l of x_N's bounds
                 lmax = fmax(lmax, fabs(lamr));
                 if (lx) sD[N * NX + rx] = lamr;   // lam_k replaces d_k (read one stage earlier)
             }
@@ -824,6 +829,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 load_acol(k, nacol);
                 const double xk = sX[k * NX + rx], trm = tr[(k - 1) * NX + rx], dk = sD[k * NX + rx];
                 nqe = Qr * (dk + (xk - trm));
+                if constexpr (XB) nqe += sZg[(k - 1) * NY + rx];   // z_u - z_l of x_k's bounds (masked by lxf)
             };
             // stage k >= 1: lam_k from lam_{k+1}; PREFETCH: load stage k - 1's operands (k >= 2)
             auto stage = [&](int k, auto prefetch_c) {
@@ -865,6 +871,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     const double uk = sU[k * NU + c], um = k == 0 ? up[c] : sU[(k - 1) * NU + c];
                     g = fma(R[c], uk - um, fma(Rm[c], uk, g));
                     if (k < N - 1) g -= R[c] * (sU[(k + 1) * NU + c] - uk);
+                    if constexpr (XB) g += sZg[k * NY + NX + c];   // reduced Lagrangian gradient
                     if constexpr (!BOUNDED) {
                         gmax = fmax(gmax, fabs(2.0 * g));
                     } else {   // projected gradient; epsilon-active holds of the first QP solve (oracle solve_one)
@@ -900,6 +907,12 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
             for (int j = 0; j < NS; ++j) Prow[j] = j < NX ? qoh[j] : 0.0;   // P~_N = blkdiag(Q, 0)
             pvr = Qr * (lx ? sX[N * NX + rx] - tr[(N - 1) * NX + rx] : 0.0);   // Q (x_N - r_{N-1})
+            if constexpr (XB) {   // barrier at x_N: Sigma on the diagonal, b in p~
+                const double sgN = sSg[(N - 1) * NY + rx], bbN = sBb[(N - 1) * NY + rx];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) Prow[j] = fma(dgx[j], sgN, Prow[j]);
+                pvr = fma(lxm, bbN, pvr);
+            }
             // (the sweep is issue-bound: its LDS operands are read in place; a prefetch buffer spills to AGPRs)
             // stage k; LAST = (k == 0), peeled so that the stages k >= 1 carry no k == 0 selects or branches
             auto stage = [&](int k, auto last_c, Wb& wb) {
@@ -961,12 +974,16 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         for (int s2 = 0; s2 < NA; ++s2) t = fma(hFu[s2 * NU + a], Tb[NQ + s2][b], t);
                         if (a == b) t += R[a] + Rm[a];
                         if constexpr (EXACT) t += wu[a * NU + b];
+                        if constexpr (XB) {
+                            if (a == b) t += sSg[k * NY + NX + a];   // barrier Sigma of u_k
+                        }
                         Hww[a][b] = t;
                         Hww[b][a] = t;
                     }
                     double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], mvb[NX + a]));
 #pragma unroll
                     for (int s2 = 0; s2 < NA; ++s2) t = fma(hFu[s2 * NU + a], mvb[NQ + s2], t);
+                    if constexpr (XB) t += sBb[k * NY + NX + a];   // barrier gradient b of u_k
                     hw[a] = t;
                 }
                 // column r of Y = [H_wx | -R | .]: x-lanes (A^T T)[r], u-lanes -R e_{r-NX}
@@ -1017,7 +1034,54 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 }
                 // Kcol = H_ww^-1 Ycol (this lane's column of K~), kff = H_ww^-1 h_w (redundant)
                 double Kcol[NU], kff[NU], Ku[NU][NU];
-                if constexpr (NU == 2) {
+                // XB: Cholesky H_ww = L L^T, Ytil = L^-1 Ycol (this lane's column of L^-1 [H_wx | -R]), htil = L^-1 h_w;
+                // the update P~ -= Ytil^T Ytil stays positive semidefinite under the barrier's large Sigma
+                double Ytil[NU], htil[NU];
+                if constexpr (XB) {
+                    double Ld[NU][NU], il[NU];
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        double sd = Hww[a][a];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) sd = fma(-Ld[a][q], Ld[a][q], sd);
+                        fact_ok &= (sd > 0.0) && isfinite(sd);
+                        const double sp = fmax(sd, 1e-300);
+                        double rr = __builtin_amdgcn_rsq(sp);
+                        rr = rr * fma(-0.5 * sp * rr, rr, 1.5);
+                        rr = rr * fma(-0.5 * sp * rr, rr, 1.5);
+                        Ld[a][a] = sp * rr;
+                        il[a] = rr;
+#pragma unroll
+                        for (int b = a + 1; b < NU; ++b) {
+                            double t = Hww[a][b];
+#pragma unroll
+                            for (int q = 0; q < a; ++q) t = fma(-Ld[b][q], Ld[a][q], t);
+                            Ld[b][a] = t * il[a];
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {   // forward substitutions
+                        double t = Ycol[a], th = hw[a];
+#pragma unroll
+                        for (int q = 0; q < a; ++q) {
+                            t = fma(-Ld[a][q], Ytil[q], t);
+                            th = fma(-Ld[a][q], htil[q], th);
+                        }
+                        Ytil[a] = t * il[a];
+                        htil[a] = th * il[a];
+                    }
+#pragma unroll
+                    for (int a = NU - 1; a >= 0; --a) {   // back substitutions: K~ column, kff
+                        double t = Ytil[a], th = htil[a];
+#pragma unroll
+                        for (int q = a + 1; q < NU; ++q) {
+                            t = fma(-Ld[q][a], Kcol[q], t);
+                            th = fma(-Ld[q][a], kff[q], th);
+                        }
+                        Kcol[a] = t * il[a];
+                        kff[a] = th * il[a];
+                    }
+                } else if constexpr (NU == 2) {
                     const double det = fma(Hww[0][0], Hww[1][1], -Hww[0][1] * Hww[0][1]);
                     fact_ok &= (Hww[0][0] > 0.0) && (det > 0.0) && isfinite(det);
                     const double idet = rcp_nr(det);
@@ -1110,7 +1174,31 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 at_mul<NQ, NA, double>(h, hFq, hFqd, Ur, Pn);
                 // x-lanes A^T mv + Q (x_k - r_{k-1}), u-lanes -R (u_k - u_{k-1}), idle lanes 0 -- blended with the
                 // lane-role factor (Rr = 0 off the u-lanes) instead of a branch
-                const double pn = fma(-Rr, duu, lxm * fma(Qr, exr, colA(mv, acol, mvb)));
+                double pn = fma(-Rr, duu, lxm * fma(Qr, exr, colA(mv, acol, mvb)));
+                double sgk = 0.0;   // XB: barrier Sigma and b of x_k (stage k-1's y)
+                if constexpr (XB) {
+                    sgk = sSg[(k - 1) * NY + rx];
+                    pn = fma(lxm, sBb[(k - 1) * NY + rx], pn);
+                }
+                if constexpr (XB) {   // P~_k = blkdiag(A^T P_xx A + Q + Sigma, R) - Ytil^T Ytil, p~_k = pn - Ytil^T htil
+                    double Yb[NU][NS];
+                    sfor<0, NS>([&](auto I) {
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) Yb[a][I] = row_bcast<I>(Ytil[a]);
+                    });
+#pragma unroll
+                    for (int j = 0; j < NS; ++j) {
+                        double v = j < NX ? fma(dgx[j], sgk, Pn[j] + qoh[j]) : rdg[j - NX];
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) v = fma(-Ytil[a], Yb[a][j], v);
+                        Prow[j] = v;
+                    }
+                    double pv2 = pn;
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) pv2 = fma(-Ytil[a], htil[a], pv2);
+                    pvr = pv2;
+                    return;
+                }
                 // K~ columns of the other lanes
                 double Kb[NU][NX];
                 sfor<0, NX>([&](auto I) {

@@ -132,13 +132,14 @@ def test_auto_solver_policy(tmp_path, model_json, mmpc_mod):
 
 
 def test_hessian_policy(tmp_path, model_json, mmpc_mod):
-    """mmpc_opts.hessian (include/mmpc.h) resolved without a GPU: AUTO = exact for nonlinear 2-link solves on the
-    group kernel, with or without control bounds (the held controls are fixed in the exact QP, DESIGN.md 3b);
-    Gauss-Newton for state-bounded / linear / exo / lane-kernel solves; EXACT where unsupported is an API error."""
+    """mmpc_opts.hessian (include/mmpc.h) resolved without a GPU: AUTO = exact for unbounded nonlinear 2-link solves
+    on the group kernel, Gauss-Newton for control-bounded (faster there) / state-bounded / linear /
+    exo / lane-kernel solves; EXACT with control bounds is supported (the held controls fixed in the exact QP);
+    EXACT where unsupported is an API error."""
     m = mmpc_mod
     s = m.Solver(model_json(N=30))
     assert s.hessian_for(4096) == m.HESSIAN_EXACT and s.hessian_for(64) == m.HESSIAN_EXACT
-    assert s.hessian_for(4096, u_bounded=True) == m.HESSIAN_EXACT
+    assert s.hessian_for(4096, u_bounded=True) == m.HESSIAN_GAUSS_NEWTON
     assert s.hessian_for(65536) == m.HESSIAN_GAUSS_NEWTON                 # lane kernel
     s.set_state_bounds([-np.inf, -np.inf, -1.5, -1.5], [np.inf, np.inf, 1.5, 1.5])
     assert s.hessian_for(4096) == m.HESSIAN_GAUSS_NEWTON                  # state bounds: interior point, GN

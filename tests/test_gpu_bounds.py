@@ -1,8 +1,9 @@
 """GPU: box-constrained controls (SURVEY.md 8a A1 bounds, ModelControl.cpp:37-50,146-157; 8f rank 1) on all
 three KKT solvers, through the C-ABI.
 
-The kernels run the oracle's projected Gauss-Newton SQP (oracle/mmpc_oracle.c solve_one; sqp_wave.h "box
-constraints").  Tolerances:
+The kernels run the oracle's projected SQP (oracle/mmpc_oracle.c solve_one; sqp_wave.h "box constraints") with
+the Hessian the solver resolves (mmpc_resolve_hessian: exact on the 16-lane group kernel, Gauss-Newton elsewhere);
+every oracle comparison runs that same Hessian (oracle_lib.solve_batch(solver=s)).  Tolerances:
   * vs the scipy bounded golden (independent solver, tests/golden/make_golden_bounds.py): V* within 1e-8
     relative, identical active sets, every control inside its box exactly;
   * vs the oracle (same algorithm): as test_gpu_parity._compare (V* 1e-9 where iteration counts agree);
@@ -72,9 +73,9 @@ def test_bounded_two_link_vs_oracle(solver, bound, mmpc_mod, oracle, tmp_path):
     x0, up, tr = oracle.synth(20250213, 500, B, N, H)
     w = np.array(WEIGHTS_CFG)
     lb, ub = [-bound, -0.8 * bound], [0.9 * bound, bound]
-    r = _solver(tmp_path, mmpc_mod, "two_link_arm", N, _kkt(mmpc_mod, solver)).solve_batch_host(
-        x0, up, tr, w, u_lb=lb, u_ub=ub)
-    o = oracle.solve_batch(N, H, x0, up, tr, w, u_lb=lb, u_ub=ub)
+    s = _solver(tmp_path, mmpc_mod, "two_link_arm", N, _kkt(mmpc_mod, solver))
+    r = s.solve_batch_host(x0, up, tr, w, u_lb=lb, u_ub=ub)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, u_lb=lb, u_ub=ub, solver=s)   # the Hessian s resolves (exact: group)
     assert (o["status"] == 0).all()
     _compare(r, o)   # V* within 1e-10 (measured <= 1.2e-15, profiles/r02/gpu_vs_oracle_agreement_v1.log)
     U = _u(r["V"], N, 4, 2)
@@ -85,9 +86,9 @@ def test_bounded_two_link_vs_oracle(solver, bound, mmpc_mod, oracle, tmp_path):
 def test_bounded_exo_vs_oracle(solver, N, B, mmpc_mod, oracle, tmp_path):
     x0, up, tr = oracle.synth(20250213, 900, B, N, H, model=oracle.EXO)
     lb, ub = [-0.5, -1.0, -0.5, -0.3], [0.6, 0.5, 1.0, 0.3]
-    r = _solver(tmp_path, mmpc_mod, "exo_arm", N, _kkt(mmpc_mod, solver)).solve_batch_host(
-        x0, up, tr, W_EXO, u_lb=lb, u_ub=ub)
-    o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, u_lb=lb, u_ub=ub, model=oracle.EXO)
+    s = _solver(tmp_path, mmpc_mod, "exo_arm", N, _kkt(mmpc_mod, solver))
+    r = s.solve_batch_host(x0, up, tr, W_EXO, u_lb=lb, u_ub=ub)
+    o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, u_lb=lb, u_ub=ub, model=oracle.EXO, solver=s)
     assert (o["status"] == 0).all()
     _compare(r, o)
 
@@ -120,7 +121,7 @@ def test_bounded_kernel_with_infinite_device_bounds(solver, mmpc_mod, oracle, tm
     ub = torch.tensor([np.inf, 1e31], **f)
     s.solve_batch(B, *t, V, st, None, None, u_lb=lb, u_ub=ub)
     torch.cuda.synchronize()
-    o = oracle.solve_batch(N, H, x0, up, tr, w)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, solver=s)
     assert (st.cpu().numpy() == 0).all()
     assert np.abs(V.cpu().numpy() - o["V"]).max() <= 1e-8 * np.abs(o["V"]).max()
 
@@ -136,12 +137,12 @@ def test_warm_start_outside_the_box(solver, mmpc_mod, oracle, tmp_path):
     lb, ub = [-2, -2], [2, 2]
     s = _solver(tmp_path, mmpc_mod, "two_link_arm", N, _kkt(mmpc_mod, solver))
     r = s.solve_batch_host(x0, up, tr, w, V=V, u_lb=lb, u_ub=ub)
-    o = oracle.solve_batch(N, H, x0, up, tr, w, V=V, u_lb=lb, u_ub=ub)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, V=V, u_lb=lb, u_ub=ub, solver=s)
     np.testing.assert_array_equal(r["status"], o["status"])
     assert (r["status"] == 3).all()
     V[:, [6 * k + 5 for k in range(N)]] = -40.0
     r = s.solve_batch_host(x0, up, tr, w, V=V, u_lb=lb, u_ub=ub)
-    ref = oracle.solve_batch(N, H, x0, up, tr, w, u_lb=lb, u_ub=ub)
+    ref = oracle.solve_batch(N, H, x0, up, tr, w, u_lb=lb, u_ub=ub, solver=s)
     assert (r["status"] == 0).all()
     assert np.abs(r["V"] - ref["V"]).max() <= 1e-8 * np.abs(ref["V"]).max()
 
@@ -187,3 +188,21 @@ def test_rank0_batch_api_single_process(mmpc_mod, oracle, tmp_path):
     h = s.solve_batch_host(x0, up, tr, np.array(WEIGHTS_CFG), u_lb=[-2.0, -2.0], u_ub=[2.0, 2.0])
     np.testing.assert_array_equal(r["V"].cpu().numpy(), h["V"])
     np.testing.assert_array_equal(r["status"].cpu().numpy(), h["status"])
+
+
+@pytest.mark.parametrize("bound", [2.0, 1e-3])
+def test_bounded_exact_hessian_vs_oracle(bound, mmpc_mod, oracle, tmp_path):
+    """mmpc_opts.hessian = EXACT with control bounds (the group kernel's BOUNDED + EXACT instantiation): the held
+    controls are fixed in the exact QP, as the oracle's solve_one (oracle_set_exact_bounded); same iterates."""
+    N, B = 30, 256
+    x0, up, tr = oracle.synth(20250213, 500, B, N, H)
+    w = np.array(WEIGHTS_CFG)
+    lb, ub = [-bound, -0.8 * bound], [0.9 * bound, bound]
+    s = _solver(tmp_path, mmpc_mod, "two_link_arm", N, mmpc_mod.KKT_RICCATI_GROUP, hessian=mmpc_mod.HESSIAN_EXACT)
+    assert s.hessian_for(B, True) == mmpc_mod.HESSIAN_EXACT
+    r = s.solve_batch_host(x0, up, tr, w, u_lb=lb, u_ub=ub)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, u_lb=lb, u_ub=ub, solver=s)
+    assert (o["status"] == 0).all()
+    _compare(r, o)
+    U = _u(r["V"], N, 4, 2)
+    assert (U >= np.array(lb)).all() and (U <= np.array(ub)).all()

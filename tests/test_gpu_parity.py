@@ -223,14 +223,14 @@ def test_per_instance_weights(model_json, mmpc_mod, oracle):
 
 
 def test_bounds_enforced(model_json, mmpc_mod, oracle):
-    """u bounds are enforced (projected GN-SQP; tests/test_gpu_bounds.py covers them in depth)"""
+    """u bounds are enforced (projected SQP; tests/test_gpu_bounds.py covers them in depth)"""
     x0, up, tr = oracle.synth(20250213, 0, 32, 30, H)
     s = mmpc_mod.Solver(model_json())
     w = np.array(WEIGHTS_CFG)
     r = s.solve_batch_host(x0, up, tr, w, u_lb=[-1e31, -1e31], u_ub=[1e31, 1e31])
     assert (r["status"] == 0).all()
     r = s.solve_batch_host(x0, up, tr, w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
-    o = oracle.solve_batch(30, H, x0, up, tr, w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
+    o = oracle.solve_batch(30, H, x0, up, tr, w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3], solver=s)
     _compare(r, o)
     assert (r["status"] == 0).all()
     assert np.abs(r["V"][:, [6 * k + 4 + c for k in range(30) for c in range(2)]]).max() <= 1e-3

@@ -232,7 +232,7 @@ def test_riccati_weights_bounds_nonfinite_warmstart(exo_solver, oracle):
     np.testing.assert_array_equal(r2["V"], r["V"])
     lb, ub = [-1e-3] * 4, [1e-3] * 4                             # bounds enforced
     r3 = s.solve_batch_host(x0[:8], up[:8], tr[:8], W_EXO, u_lb=lb, u_ub=ub)
-    o3 = oracle.solve_batch(N, H, x0[:8], up[:8], tr[:8], W_EXO, u_lb=lb, u_ub=ub, model=oracle.EXO)
+    o3 = oracle.solve_batch(N, H, x0[:8], up[:8], tr[:8], W_EXO, u_lb=lb, u_ub=ub, model=oracle.EXO, solver=s)
     np.testing.assert_array_equal(r3["status"], o3["status"])
     x0b, trb = x0[:4].copy(), tr[:4].copy()                      # non-finite inputs
     x0b[1, 2] = np.nan
@@ -301,7 +301,7 @@ def test_group_kernel_linear_weights_bounds_nonfinite_warmstart(model_json, mmpc
     assert (r2["iters"] == 0).all() and (r2["status"] == 0).all()
     np.testing.assert_array_equal(r2["V"], r["V"])
     r3 = s.solve_batch_host(x0[:8], up[:8], tr[:8], w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
-    o3 = oracle.solve_batch(30, H, x0[:8], up[:8], tr[:8], w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3])
+    o3 = oracle.solve_batch(30, H, x0[:8], up[:8], tr[:8], w, u_lb=[-1e-3, -1e-3], u_ub=[1e-3, 1e-3], solver=s)
     np.testing.assert_array_equal(r3["status"], o3["status"])
     x0b, trb = x0[:4].copy(), tr[:4].copy()
     x0b[1, 0] = np.nan

@@ -94,7 +94,7 @@ def test_generated_model_bounded(mmpc_mod, oracle):
     w = weights(s.nx, s.nu)
     lb, ub = np.array([-1.5]), np.array([1.5])
     g = s.solve_batch_host(x0, up, tr, w, u_lb=lb, u_ub=ub)
-    o = oracle.solve_batch(s.N, s.h, x0, up, tr, w, model=mid, u_lb=lb, u_ub=ub)
+    o = oracle.solve_batch(s.N, s.h, x0, up, tr, w, model=mid, u_lb=lb, u_ub=ub, solver=s)
     compare(g, o, tight=1e-8)
     U = g["V"][:, :-s.nx].reshape(64, s.N, s.nx + s.nu)[:, :, s.nx:]
     assert U.min() >= -1.5 and U.max() <= 1.5
