@@ -6,7 +6,7 @@ the Hessian the solver resolves (mmpc_resolve_hessian: exact on the 16-lane grou
 every oracle comparison runs that same Hessian (oracle_lib.solve_batch(solver=s)).  Tolerances:
   * vs the scipy bounded golden (independent solver, tests/golden/make_golden_bounds.py): V* within 1e-8
     relative, identical active sets, every control inside its box exactly;
-  * vs the oracle (same algorithm): as test_gpu_parity._compare (V* 1e-9 where iteration counts agree);
+  * vs the oracle (same algorithm): as test_gpu_parity._compare (V* 1e-10 where iteration counts agree);
     the Riccati solvers solve the same equality-constrained QPs by a different factorisation, 1e-8;
   * infinite bounds through the host API select the unbounded kernels: bitwise the unbounded result.
 """

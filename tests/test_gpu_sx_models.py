@@ -4,7 +4,7 @@ Each generated <name>.so (mahi-mpc_amd/lib/user, built by __graft_entry__.build(
 kernels compiled for that model; mmpc.Solver / ModelControl load it through the JSON's dll_filepath, as the
 reference loads <name>.so (ModelControl.cpp:62, ModelGenerator.cpp:254-259).  Checked against:
   * the oracle's GN-SQP on the same dynamics (host build of the same generated header, itself pinned to sympy
-    in tests/test_sx_models.py): V* within 1e-9 relative where the iteration counts agree (>= 90 %), 1e-6
+    in tests/test_sx_models.py): V* within 1e-10 relative where the iteration counts agree (>= 90 %), 1e-6
     everywhere (a stop test landing within roundoff of its threshold), every instance converged;
   * for the reference's double pendulum, the built-in 2-link kernels of libmmpc.so on cfg#2-recipe instances;
   * every KKT solver the generated library has (16-lane group Riccati, lane Riccati), bounded controls,
@@ -40,7 +40,7 @@ def weights(nx, nu):
     return np.concatenate([np.full(nx, 5.0), np.full(nu, 0.5), np.full(nu, 0.01)])
 
 
-def compare(g, o, tight=1e-9):
+def compare(g, o, tight=1e-10):
     assert (g["status"] == 0).all(), np.bincount(g["status"])
     assert (o["status"] == 0).all()
     same = g["iters"] == o["iters"]
