@@ -303,14 +303,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     int status = ST_MAX_ITER;
     int it = 0;
     double kkt = 0.0, mu = 0.0, pg_prev = INFINITY;
+    constexpr bool FUSE_TRIAL = !BOUNDED && !XB;  // the alpha = 1 trial is evaluated inside the step sweep
+    // FUSE_FWD (fp64 factor): the step sweep evaluates the alpha = 1 trial point with its Jacobian and forms there
+    // everything pass (1) of the next iteration computes at that point (defects, d, J, |c|_1, max|c|), so when the
+    // full step is accepted (99.7 % of the cfg#3 iterations, every one after the first: tools/alpha_stats.py) the
+    // next iteration starts at (2).  This saves the value-only trial evaluation and pass (1)'s sweep (cfg#3:
+    // 11.63 -> 11.20 ms); the fp32-factor build (cfg#5) spills more with it (10.05 -> 11.77 ms) and keeps the
+    // separate pass.  fwd_ready: C and D of the workspace hold the accepted iterate's values.
+    constexpr bool FUSE_FWD = FUSE_TRIAL && std::is_same<FT, double>::value;
+    bool fwd_ready = false;
+    double J0n = 0.0, c1n = 0.0, cmaxn = 0.0;
+    bool nfn = false;
     MMPC_PHASE(0);
     #pragma unroll 1
     for (it = 0; it <= p.max_iter; ++it) {
         // ---- (1) forward: F, defects, d_{k+1} = A_k d_k + c_k, merit value ----
-        double J0 = 0.0, c1 = 0.0, cmax = 0.0;
+        double J0 = J0n, c1 = c1n, cmax = cmaxn;
         double lsum = 0.0, cmpl0 = 0.0, cmplmu = 0.0;  // interior point: sum log s, max |s z|, max |s z - mu|
-        bool nonfinite = false;
-        {
+        bool nonfinite = nfn;
+        if (!(FUSE_FWD && fwd_ready)) {
+            J0 = 0.0;
+            c1 = 0.0;
+            cmax = 0.0;
+            nonfinite = false;
             // software pipeline: the model inputs of stage k+1 are loaded during stage k (one wave per SIMD
             // has no other wave to hide HBM latency behind); the other loads of a stage are issued before
             // its model evaluation, which covers them
@@ -382,9 +397,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         double gmax = 0.0, lmax = 0.0, dJ = 0.0;
         double mub_next = mub, amax = 1.0, az = 1.0, dbar = 0.0;  // interior point (XB)
         bool fact_ok = true, done = false;
+        fwd_ready = false;
         const double beps = BOUNDED ? fmin(kBoundEps, pg_prev) : 0.0;
-        constexpr bool FUSE_TRIAL = !BOUNDED && !XB;  // the alpha = 1 trial is evaluated inside the step sweep
-        double Jt1 = 0.0, ct1 = 0.0;
+        double Jt1 = 0.0, ct1 = 0.0, cmt1 = 0.0;
+        bool nft1 = false;
         // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
         double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
         #pragma unroll 1
@@ -806,6 +822,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             dJ = 0.0;
             Jt1 = 0.0;
             ct1 = 0.0;
+            cmt1 = 0.0;
+            nft1 = false;
             amax = 1.0;
             az = 1.0;
             dbar = 0.0;
@@ -823,9 +841,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 }
                 // software pipeline as in (1); the feedback gains K_k are consumed (and loaded) before the model
                 // evaluation, whose compute then covers the remaining loads of the stage
-                double xpf[NX], upf[NU], umt[NU];
+                double xpf[NX], upf[NU], umt[NU], dt[NX];  // dt: d of the alpha = 1 trial point (FUSE_FWD)
 #pragma unroll
-                for (int r = 0; r < NX; ++r) xpf[r] = ST(0, SF::X, r);
+                for (int r = 0; r < NX; ++r) {
+                    xpf[r] = ST(0, SF::X, r);
+                    dt[r] = 0.0;
+                }
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
                     upf[c] = ST(0, SF::U, c);
@@ -923,21 +944,41 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         dup[c] = du[c];
                     }
                     if constexpr (FUSE_TRIAL) {   // trial point (x_k + dx_k, u_k + du_k), its defect to x_{k+1} + dx_{k+1}
+                        // = pass (1) at the iterate the full step gives (the update's fma(1, dx, x) is x + dx): the
+                        // same expressions in the same order, C_k and d_{k+1} stored for the next iteration (C_k of
+                        // this iteration was read above; a rejected full step recomputes both in (1))
                         double xt[NX], ut[NU], xdt[NX];
 #pragma unroll
                         for (int r = 0; r < NX; ++r) xt[r] = x[r] + dxk[r];
 #pragma unroll
                         for (int c = 0; c < NU; ++c) ut[c] = u[c] + du[c];
-                        {
+                        if constexpr (FUSE_FWD) {
+                            double tFq[SQ], tFqd[NA * NA], tFu[NA * NU], dn[NX];
+                            STAGE_EVAL(xt, ut, xdt, tFq, tFqd, tFu, true);
+                            a_mul<NQ, NA>(h, tFq, tFqd, dt, dn);
+#pragma unroll
+                            for (int r = 0; r < NX; ++r) {
+                                const double F = fma(h, xdt[r], xt[r]);
+                                const double c = F - (xpf[r] + dx[r]);
+                                SK(0, SF::C, r) = c;
+                                cmt1 = fmax(cmt1, fabs(c));
+                                ct1 += fabs(c);
+                                nft1 |= !isfinite(c);
+                                const double er = F - rk[r];
+                                Jt1 = fma(er * Q[r], er, Jt1);
+                                dt[r] = dn[r] + c;
+                                SK(1, SF::D, r) = dt[r];
+                            }
+                        } else {
                             double* nil_ = nullptr;
                             STAGE_EVAL(xt, ut, xdt, nil_, nil_, nil_, false);
-                        }
 #pragma unroll
-                        for (int r = 0; r < NX; ++r) {
-                            const double F = fma(h, xdt[r], xt[r]);
-                            const double er = F - rk[r];
-                            Jt1 = fma(er * Q[r], er, Jt1);
-                            ct1 += fabs(F - (xpf[r] + dx[r]));
+                            for (int r = 0; r < NX; ++r) {
+                                const double F = fma(h, xdt[r], xt[r]);
+                                const double er = F - rk[r];
+                                Jt1 = fma(er * Q[r], er, Jt1);
+                                ct1 += fabs(F - (xpf[r] + dx[r]));
+                            }
                         }
 #pragma unroll
                         for (int c = 0; c < NU; ++c) {
@@ -1040,6 +1081,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         if (!accepted) {
             status = ST_LS_FAILED;
             break;
+        }
+        if (FUSE_FWD && alpha == 1.0) {  // the step sweep already formed pass (1) at the new iterate
+            fwd_ready = true;
+            J0n = Jt1;
+            c1n = ct1;
+            cmaxn = cmt1;
+            nfn = nft1;
         }
         if constexpr (XB) {  // y and the duals of stage k's (x_{k+1} | u_k), as oracle solve_one_ip
             #pragma unroll 1
