@@ -295,43 +295,59 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     int it = 0;
     double kkt = 0.0, mu = 0.0, pg_prev = INFINITY;
     bool done = !valid;
+    // FUSE_FWD: the line search's alpha = 1 trial evaluates the model with its Jacobian and writes everything phase A
+    // computes at that point (F_k, c_k, the stage blocks; J, |c|_1, max|c|); when the full step is accepted (every
+    // cfg#2 iteration, tools/alpha_stats.py) the next iteration skips phase A.  The trial point fma(1, d, v) is the
+    // update's iterate and the sums run in phase A's order, so the values are phase A's bit for bit.  The old stage
+    // blocks are dead once the directional derivative is formed; a rejected full step recomputes them in phase A.
+    constexpr bool FUSE_FWD = !XB;
+    bool fwd_ready = false;
+    double J0n = 0.0, c1n = 0.0, cmaxn = 0.0;
+    int nfn = 0;
     MMPC_PHASE(0);
     for (it = 0; !done; ++it) {
         MMPC_PHASE(8);
         __builtin_amdgcn_wave_barrier();
         // ---- A. stage-parallel: F_k, A_k/B_k blocks, defects, merit value ----
-        double J0 = 0.0, c1 = 0.0, cmax = 0.0;
-        int nonfinite = 0;
-        for (int k = gl; k < N; k += G) {
-            double x[NX], u[NU], xd[NX], Fq[SQ], Fqd[FD], Fu[FU];
+        double J0 = J0n, c1 = c1n, cmax = cmaxn;
+        int nonfinite = nfn;
+        const bool evalA = !(FUSE_FWD && fwd_ready);
+        if (evalA) {
+            J0 = 0.0;
+            c1 = 0.0;
+            cmax = 0.0;
+            nonfinite = 0;
+            for (int k = gl; k < N; k += G) {
+                double x[NX], u[NU], xd[NX], Fq[SQ], Fqd[FD], Fu[FU];
 #pragma unroll
-            for (int r = 0; r < NX; ++r) x[r] = sX[k * NX + r];
+                for (int r = 0; r < NX; ++r) x[r] = sX[k * NX + r];
 #pragma unroll
-            for (int c = 0; c < NU; ++c) u[c] = sU[k * NU + c];
-            group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, Fq, Fqd, Fu, true);
+                for (int c = 0; c < NU; ++c) u[c] = sU[k * NU + c];
+                group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, Fq, Fqd, Fu, true);
 #pragma unroll
-            for (int i = 0; i < FQ; ++i) sFq[k * FQ + i] = h * Fq[i];
+                for (int i = 0; i < FQ; ++i) sFq[k * FQ + i] = h * Fq[i];
 #pragma unroll
-            for (int i = 0; i < FD; ++i) sFqd[k * FD + i] = h * Fqd[i];
+                for (int i = 0; i < FD; ++i) sFqd[k * FD + i] = h * Fqd[i];
 #pragma unroll
-            for (int i = 0; i < FU; ++i) sFu[k * FU + i] = h * Fu[i];
+                for (int i = 0; i < FU; ++i) sFu[k * FU + i] = h * Fu[i];
 #pragma unroll
-            for (int r = 0; r < NX; ++r) {
-                const double F = fma(h, xd[r], x[r]);
-                sF[k * NX + r] = F;
-                const double c = F - sX[(k + 1) * NX + r];
-                sC[k * NX + r] = c;
-                cmax = fmax(cmax, fabs(c));
-                c1 += fabs(c);
-                nonfinite |= !isfinite(c);
-                const double e = F - tr[k * NX + r];
-                J0 = fma(e * Q[r], e, J0);
-            }
+                for (int r = 0; r < NX; ++r) {
+                    const double F = fma(h, xd[r], x[r]);
+                    sF[k * NX + r] = F;
+                    const double c = F - sX[(k + 1) * NX + r];
+                    sC[k * NX + r] = c;
+                    cmax = fmax(cmax, fabs(c));
+                    c1 += fabs(c);
+                    nonfinite |= !isfinite(c);
+                    const double e = F - tr[k * NX + r];
+                    J0 = fma(e * Q[r], e, J0);
+                }
 #pragma unroll
-            for (int c = 0; c < NU; ++c) {
-                const double um = (k == 0) ? up[c] : sU[(k - 1) * NU + c];
-                const double dif = u[c] - um;
-                J0 = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], J0));
+                for (int c = 0; c < NU; ++c) {
+                    const double um = (k == 0) ? up[c] : sU[(k - 1) * NU + c];
+                    const double dif = u[c] - um;
+                    J0 = fma(dif * R[c], dif, fma(u[c] * Rm[c], u[c], J0));
+                }
             }
         }
         double lsum = 0.0, cmpl0 = 0.0, cmplmu = 0.0;  // interior point: sum log s, max |s z|, max |s z - mu|
@@ -352,9 +368,12 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             cmplmu = group_max(cmplmu);
             nonfinite |= !isfinite(lsum);
         }
-        J0 = group_sum(J0);
-        c1 = group_sum(c1);
-        cmax = group_max(cmax);
+        if (evalA) {
+            J0 = group_sum(J0);
+            c1 = group_sum(c1);
+            cmax = group_max(cmax);
+        }
+        fwd_ready = false;
         __builtin_amdgcn_wave_barrier();
         MMPC_PHASE(1);
 
@@ -1538,8 +1557,11 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         const double dphi = XB ? dJ + dbar - mu * c1 : dJ - mu * c1;
         double alpha = amax;
         bool accepted = false;
-        for (int ls = 0; ls < 30; ++ls) {
-            double Jt = 0.0, ct = 0.0, lt = 0.0;
+        // the alpha = 1 trial with the Jacobian (FUSE_FWD): ctm, nft are phase A's max|c| and nonfinite flag there
+        double ctm = 0.0;
+        int nft = 0;
+        auto trial = [&](auto jac_c, double& Jt, double& ct, double& lt) {
+            constexpr bool JAC = decltype(jac_c)::value;
             for (int k = gl; k < N; k += G) {
                 double x[NX], u[NU], xd[NX];
 #pragma unroll
@@ -1549,13 +1571,36 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     u[c] = fma(alpha, sDU[k * NU + c], sU[k * NU + c]);
                     if (BOUNDED) u[c] = proj(u[c], lbv[c], ubv[c]);  // projected trial point
                 }
-                group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, nullptr, nullptr, nullptr, false);
+                if constexpr (JAC) {   // = phase A at the trial point (stored for the next iteration)
+                    double Fq[SQ], Fqd[FD], Fu[FU];
+                    group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, Fq, Fqd, Fu, true);
 #pragma unroll
-                for (int r = 0; r < NX; ++r) {
-                    const double F = fma(h, xd[r], x[r]);
-                    const double er = F - tr[k * NX + r];
-                    Jt = fma(er * Q[r], er, Jt);
-                    ct += fabs(F - fma(alpha, sDX[(k + 1) * NX + r], sX[(k + 1) * NX + r]));
+                    for (int i = 0; i < FQ; ++i) sFq[k * FQ + i] = h * Fq[i];
+#pragma unroll
+                    for (int i = 0; i < FD; ++i) sFqd[k * FD + i] = h * Fqd[i];
+#pragma unroll
+                    for (int i = 0; i < FU; ++i) sFu[k * FU + i] = h * Fu[i];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        const double F = fma(h, xd[r], x[r]);
+                        sF[k * NX + r] = F;
+                        const double c = F - fma(alpha, sDX[(k + 1) * NX + r], sX[(k + 1) * NX + r]);
+                        sC[k * NX + r] = c;
+                        ctm = fmax(ctm, fabs(c));
+                        ct += fabs(c);
+                        nft |= !isfinite(c);
+                        const double er = F - tr[k * NX + r];
+                        Jt = fma(er * Q[r], er, Jt);
+                    }
+                } else {
+                    group_model<Model>(lin, lFq, lFqd, lFu, lxd, lxs, up, x, u, xd, nullptr, nullptr, nullptr, false);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        const double F = fma(h, xd[r], x[r]);
+                        const double er = F - tr[k * NX + r];
+                        Jt = fma(er * Q[r], er, Jt);
+                        ct += fabs(F - fma(alpha, sDX[(k + 1) * NX + r], sX[(k + 1) * NX + r]));
+                    }
                 }
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
@@ -1572,6 +1617,13 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     }
                 }
             }
+        };
+        bool jac_trial = false;
+        for (int ls = 0; ls < 30; ++ls) {
+            double Jt = 0.0, ct = 0.0, lt = 0.0;
+            jac_trial = FUSE_FWD && ls == 0;   // alpha = amax = 1 without state bounds
+            if (jac_trial) trial(std::true_type{}, Jt, ct, lt);
+            else trial(std::false_type{}, Jt, ct, lt);
             Jt = group_sum(Jt);
             ct = group_sum(ct);
             if (XB) lt = group_sum(lt);
@@ -1580,6 +1632,13 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise ||
                 (!XB && it == 0 && first_iter_filter_accepts(J0, c1, Jt, ct, dJ, alpha))) {
                 accepted = true;
+                if (FUSE_FWD && jac_trial) {   // the next iteration starts after phase A
+                    fwd_ready = true;
+                    J0n = Jt;
+                    c1n = ct;
+                    cmaxn = group_max(ctm);
+                    nfn = nft;
+                }
                 break;
             }
             alpha *= 0.5;
