@@ -788,24 +788,26 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         auto d_recursion_dist = [&]() {
             double dr = 0.0;
             if (lx) sD[rx] = 0.0;
-            double na[NX], nc;
-            {
-                double nb[NU];
-                load_arow(0, na, nb);
-                nc = sC[rx];
-            }
-#pragma unroll 2
-            for (int k = 0; k < N; ++k) {
+            // stage operands as loaded (the blend with the lane-role factors happens at the use, so the wait for a
+            // load sits a full stage after its issue): two buffers, each refilled two stages ahead
+            struct Op {
+                double q[NQ > 0 ? NQ : 1], d[NA], c;
+            };
+            auto fetch = [&](int k, Op& o) {
+#pragma unroll
+                for (int s2 = 0; s2 < NQ; ++s2) o.q[s2] = sFq[k * FQ + ta * NQ + s2];
+#pragma unroll
+                for (int s2 = 0; s2 < NA; ++s2) o.d[s2] = sFqd[k * FD + ta * NA + s2];
+                o.c = sC[k * NX + rx];
+            };
+            auto stage = [&](int k, Op& o) {
                 double db[NX], arow[NX];
 #pragma unroll
-                for (int j = 0; j < NX; ++j) arow[j] = na[j];
-                const double cr = nc;
-                {
-                    const int kn = k + 1 < N ? k + 1 : k;
-                    double nb[NU];
-                    load_arow(kn, na, nb);
-                    nc = sC[kn * NX + rx];
-                }
+                for (int s2 = 0; s2 < NQ; ++s2) arow[s2] = fma(lad, o.q[s2], hrow[s2]);
+#pragma unroll
+                for (int s2 = 0; s2 < NA; ++s2) arow[NQ + s2] = fma(lad, o.d[s2], hrow[NQ + s2]);
+                const double cr = o.c;
+                fetch(k + 2 < N ? k + 2 : N - 1, o);   // unconditional: static wait counts
                 sfor<0, NX>([&](auto I) { db[I] = row_bcast<I>(dr); });
                 double t0 = dr + cr, t1 = 0.0;
 #pragma unroll
@@ -815,7 +817,16 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 }
                 dr = lxf * (t0 + t1);
                 if (lx) sD[(k + 1) * NX + rx] = dr;
+            };
+            Op o0, o1;
+            fetch(0, o0);
+            fetch(N > 1 ? 1 : 0, o1);
+            int k = 0;
+            for (; k + 1 < N; k += 2) {
+                stage(k, o0);
+                stage(k + 1, o1);
             }
+            if (k < N) stage(k, o0);
         };
         // adjoint + reduced gradient + Riccati backward sweep; lane r: row r of P~ (Prow) and p~ (pvr), lam[r]
         // column r of the a-rows of A at stage k: hFq[:, r] (q-lanes), hFqd[:, r - NQ] (a-lanes), 0 otherwise
@@ -842,22 +853,34 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 lmax = fmax(lmax, fabs(lamr));
                 if (lx) sD[N * NX + rx] = lamr;   // lam_k replaces d_k (read one stage earlier)
             }
-            // stage operands (loaded one stage ahead): column r of A's a-rows, Q (d_k + x_k - r_{k-1})[r]
-            double nacol[NA], nqe = 0.0;
-            auto load = [&](int k) {   // k >= 1
-                load_acol(k, nacol);
-                const double xk = sX[k * NX + rx], trm = tr[(k - 1) * NX + rx], dk = sD[k * NX + rx];
-                nqe = Qr * (dk + (xk - trm));
-                if constexpr (XB) nqe += sZg[(k - 1) * NY + rx];   // z_u - z_l of x_k's bounds (masked by lxf)
+            // stage operands as loaded, two buffers refilled two stages ahead (d_k is read before stage k writes lam_k
+            // over it): column r of A's a-rows and the pieces of Q (d_k + x_k - r_{k-1})[r], combined at the use
+            struct Op {
+                double fd[NA], fq[NA], xk, trm, dk, zg;
             };
-            // stage k >= 1: lam_k from lam_{k+1}; PREFETCH: load stage k - 1's operands (k >= 2)
-            auto stage = [&](int k, auto prefetch_c) {
-                constexpr bool PREFETCH = decltype(prefetch_c)::value;
+            auto fetch = [&](int k, Op& o) {   // k >= 1
+#pragma unroll
+                for (int t2 = 0; t2 < NA; ++t2) {
+                    o.fd[t2] = sFqd[k * FD + t2 * NA + ta];
+                    if constexpr (NQ > 0) o.fq[t2] = sFq[k * FQ + t2 * NQ + rq];
+                }
+                o.xk = sX[k * NX + rx];
+                o.trm = tr[(k - 1) * NX + rx];
+                o.dk = sD[k * NX + rx];
+                if constexpr (XB) o.zg = sZg[(k - 1) * NY + rx];   // z_u - z_l of x_k's bounds (masked by lxf)
+            };
+            // stage k >= 1: lam_k from lam_{k+1}; then refill o with stage k - 2 (k >= 3)
+            auto stage = [&](int k, Op& o) {
                 double acol[NA];
 #pragma unroll
-                for (int s2 = 0; s2 < NA; ++s2) acol[s2] = nacol[s2];
-                const double qe = nqe;
-                if constexpr (PREFETCH) load(k - 1);
+                for (int t2 = 0; t2 < NA; ++t2) {
+                    double v = lad * o.fd[t2];
+                    if constexpr (NQ > 0) v = fma(lqd, o.fq[t2], v);
+                    acol[t2] = v;
+                }
+                double qe = Qr * (o.dk + (o.xk - o.trm));
+                if constexpr (XB) qe += o.zg;
+                fetch(k >= 3 ? k - 2 : 1, o);   // unconditional: static wait counts
                 double lamb[NX];
                 sfor<0, NX>([&](auto I) { lamb[I] = row_bcast<I>(lamr); });
                 // (A^T lam)[r] + Q e_{k-1}[r], two partial sums
@@ -874,9 +897,15 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 if (lx) sD[k * NX + rx] = lamr;
             };
             if (N >= 2) {
-                load(N - 1);
-                for (int k = N - 1; k >= 2; --k) stage(k, std::true_type{});
-                stage(1, std::false_type{});
+                Op o0, o1;
+                fetch(N - 1, o0);
+                fetch(N >= 3 ? N - 2 : 1, o1);
+                int k = N - 1;
+                for (; k >= 2; k -= 2) {
+                    stage(k, o0);
+                    stage(k - 1, o1);
+                }
+                if (k == 1) stage(1, o0);
             }
             // the lam rows of the other lanes of this wave must be visible to the gradient pass
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
