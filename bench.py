@@ -160,7 +160,7 @@ def _cpu_leg(o, cfg, N, h, target_s, kw, kkt):
 
 
 def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, hessian=1, u_bound=None,
-                 x_bound=None):
+                 x_bound=None, kkt_solver=0):
     """The oracle (oracle/liboracle.so: the same NLP and SQP in plain C + OpenMP, cold start V = 0) timed on a
     bounded sample of the same seeded workload, in two legs:
       riccati          the Riccati recursion the GPU kernels run (ORACLE_KKT_RICCATI: same algorithm, same iterates)
@@ -176,7 +176,8 @@ def cpu_baseline(cfg, N, h, target_s, gpu_V, gpu_iters, tol_grad, tol_defect, he
               hessian=o.HESS_EXACT if hessian == 2 else o.HESS_GAUSS_NEWTON)
     nu = cfg["nu"]
     if u_bound is not None:   # the oracle's projected GN-SQP (its Riccati restatement covers unbounded solves only)
-        kw.update(u_lb=np.full(nu, -u_bound), u_ub=np.full(nu, u_bound))
+        # with the active-set rule of the kernel that ran (the 16-lane kernel also releases holds)
+        kw.update(u_lb=np.full(nu, -u_bound), u_ub=np.full(nu, u_bound), bound_release=kkt_solver == 3)
     if x_bound is not None:   # the oracle's interior-point variant (solve_one_ip, dense)
         half = cfg["nx"] // 2
         kw.update(x_lb=np.array([-np.inf] * half + [-x_bound] * half), x_ub=np.array([np.inf] * half + [x_bound] * half))
@@ -497,7 +498,7 @@ def run_config(args, name, world, rank, primary=True):
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin and name != "cfg5":
         out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
                                            tol_defect, hess, None if ulb is None else args.u_bound,
-                                           args.x_bound if primary else None)
+                                           args.x_bound if primary else None, ksolver)
     if hbuf:
         for hb in hbuf:
             hb.close()

@@ -38,9 +38,10 @@ __host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int nq, int 
 // exact Hessian (EXACT): per stage the x rows of W_k = h sum_s lam_{k+1,NQ+s} d^2 acc_s/d(x,u)^2 (nx x (nx+nu))
 // and its u-u block (nu x nu), written stage-parallel and read by the lane-distributed Riccati sweep
 __host__ __device__ constexpr int group_hess_doubles(int nx, int nu) { return nx * (nx + nu) + nu * nu; }
-// HBM workspace doubles per instance: K_k | kff_k per stage, then the W_k blocks per stage
+// HBM workspace doubles per instance: K_k | kff_k per stage, then the W_k blocks per stage, then (control-bounded
+// solves) the un-held rows [H_wx | -R | H_ww | h_w] of each stage QP, for the multipliers of the held controls
 __host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) {
-    return N * nu * (nx + nu + 1) + N * group_hess_doubles(nx, nu);
+    return N * nu * (nx + nu + 1) + N * group_hess_doubles(nx, nu) + N * nu * (nx + 2 * nu + 1);
 }
 
 struct GroupWork {
@@ -175,6 +176,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
     constexpr int KZ = NX + NU, HW = group_hess_doubles(NX, NU);
     double* const wH = wK + N * NU * (NS + 1);  // EXACT: [N][HW] = W_k x rows [NX][KZ] | W_k uu block [NU][NU]
+    constexpr int NR = NS + NU + 1;             // BOUNDED: [N][NU][NR] = un-held [H_wx | -R | H_ww | h_w] rows
+    double* const wRel = wH + N * HW;
     const double* const trg = p.traj + ii * (int64_t)N * NX;
 
     const double* w = p.weights + ii * p.w_stride;
@@ -1044,6 +1047,23 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     Ycol[a] = colA(T[a], acol, tb) - rdg[a];
                     if constexpr (EXACT) Ycol[a] += wr[NX + a];   // H_wx[a][r] += W_ux[a][r] (x-lanes; 0 else)
                 }
+                // BOUNDED: the un-held stage rows [H_wx | -R | H_ww | h_w] (lane j < NS: column j; lanes NS.. the H_ww
+                // columns and h_w, the idle lanes duplicating h_w) -- the step sweep forms the multiplier of a held
+                // control from them (primal-dual active set: release a hold whose multiplier points into the box)
+                if constexpr (BOUNDED) {
+#pragma unroll
+                    for (int c0 = 0; c0 < NR; c0 += G) {   // column c0 + r; lanes past the row rewrite its last entry
+                        const int col = c0 + r < NR ? c0 + r : NR - 1;
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) {
+                            double v = hw[a];
+#pragma unroll
+                            for (int b = 0; b < NU; ++b)
+                                if (col == NS + b) v = Hww[a][b];
+                            wRel[(k * NU + a) * NR + col] = col < NS ? Ycol[a] : v;
+                        }
+                    }
+                }
                 // held controls (BOUNDED, sHold of this QP solve): du_a = target - u_a fixed in the stage QP, as the
                 // one-lane sweep -- p~ gains [H_wx | -R]^T delta, h_w the coupling H_ww delta, the held rows and
                 // columns of H_ww become the identity and the held rows of [H_wx | -R] zero, so that K_a = 0 and
@@ -1430,13 +1450,18 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 // operands double-buffered two stages ahead (manual unroll by two, so the buffers are renamed, not
                 // copied): the K row from the HBM/L2 workspace, row r of [A - I | B] and c_k[r] from LDS
                 struct Ops {
-                    double K[NK], a[NX], b[NU], c;
+                    double K[NK], a[NX], b[NU], c, Rw[BOUNDED ? NR : 1];
                 };
+                const double* const Rp = wRel + ru * NR;   // BOUNDED: un-held row ru at Rp + k NU NR
                 auto fetch = [&](int k, Ops& o) {
 #pragma unroll
                     for (int j = 0; j < NK; ++j) o.K[j] = Kp[k * NU * NK + j];
                     load_arow(k, o.a, o.b);
                     o.c = sC[k * NX + rx];
+                    if constexpr (BOUNDED) {
+#pragma unroll
+                        for (int j = 0; j < NR; ++j) o.Rw[j] = Rp[k * NU * NR + j];
+                    }
                 };
                 auto stage = [&](int k, Ops& o) {
                     double sb[NS];
@@ -1464,9 +1489,21 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     if constexpr (BOUNDED) {
                         if (check && lu) {
                             const double hv = sHold[k * NU + ru], t = sU[k * NU + ru] + du;
-                            if (hv != hv && (t < lbr || t > ubr)) {
-                                sHold[k * NU + ru] = t < lbr ? lbr : ubr;
-                                resolve = true;
+                            if (hv != hv) {   // free: hold it where its step crosses a bound
+                                if (t < lbr || t > ubr) {
+                                    sHold[k * NU + ru] = t < lbr ? lbr : ubr;
+                                    resolve = true;
+                                }
+                            } else {   // held: release it when its multiplier H_ww du + [H_wx | -R] s + h_w points inward
+                                double m = o.Rw[NR - 1];
+#pragma unroll
+                                for (int j = 0; j < NS; ++j) m = fma(o.Rw[j], sb[j], m);
+#pragma unroll
+                                for (int b = 0; b < NU; ++b) m = fma(o.Rw[NS + b], dub[b], m);
+                                if ((hv == lbr && m < 0.0) || (hv == ubr && m > 0.0)) {
+                                    sHold[k * NU + ru] = NAN;
+                                    resolve = true;
+                                }
                             }
                         }
                     }
@@ -1519,12 +1556,15 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     if (!fact_ok) break;
                 }
                 resolve = false;
-                step_dist(BOUNDED && pass + 1 < kBoundPasses);
+                // QP solves of this iteration: two at the first (the cold start's active set moves most there, and a
+                // wave pays its slowest instance's solves), kBoundPasses later (oracle bound_release)
+                const int passes = it == 0 ? 2 : kBoundPasses;
+                step_dist(BOUNDED && pass + 1 < passes);
                 if constexpr (!BOUNDED) {
                     break;
                 } else {
                     resolve = group_max(resolve ? 1.0 : 0.0) != 0.0;
-                    if (!resolve || pass + 1 >= kBoundPasses) break;
+                    if (!resolve || pass + 1 >= passes) break;
                 }
             }
             __builtin_amdgcn_wave_barrier();

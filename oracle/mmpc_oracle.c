@@ -307,6 +307,12 @@ void oracle_set_hessian(int mode) { g_hess_mode = mode; }
 /* EXACT with control bounds: the held controls fixed in the exact QP (1), or such solves keep Gauss-Newton (0) */
 static int g_exact_bounded = 1;
 void oracle_set_exact_bounded(int on) { g_exact_bounded = on; }
+/* Control bounds, primal-dual active set (the 16-lane Riccati kernel, round 3): after each QP solve a held control
+ * whose multiplier -- the un-held QP gradient (H0 du + g0)_a at the solution -- points into the box is released as
+ * well as a free control whose step crosses a bound held (Hintermueller, Ito & Kunisch 2003); two QP solves at the
+ * first iteration, ORACLE_BOUND_PASSES later.  Off: holds are only added (the condensed and lane kernels). */
+static int g_bound_release = 0;
+void oracle_set_bound_release(int on) { g_bound_release = on; }
 
 void oracle_two_link_xdot(const double* x, const double* u, double* xdot) {
     oracle_two_link_jac(x, u, NULL, NULL, xdot);
@@ -770,10 +776,20 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
                 for (int a = 0; a < M; ++a) s->du[a] = -s->ggn[a];
                 if (chol_solve(M, s->H, s->du) != 0) { fact_fail = 1; break; }
             }
-            if (!has_b || pass + 1 >= ORACLE_BOUND_PASSES) break;
+            if (!has_b || pass + 1 >= ((g_bound_release && it == 0) ? 2 : ORACLE_BOUND_PASSES)) break;
             int added = 0;
             for (int a = 0; a < M; ++a) {
-                if (s->tgt[a] == s->tgt[a]) continue;
+                if (s->tgt[a] == s->tgt[a]) {
+                    if (g_bound_release) {   /* the hold's multiplier: release it when it points into the box */
+                        double r = s->g0[a];
+                        for (int b = 0; b < M; ++b) r += s->H0[a * M + b] * s->du[b];
+                        if ((s->tgt[a] == lbv[a % NU] && r < 0.0) || (s->tgt[a] == ubv[a % NU] && r > 0.0)) {
+                            s->tgt[a] = NAN;
+                            added = 1;
+                        }
+                    }
+                    continue;
+                }
                 const double t = s->U[a] + s->du[a];
                 if (t < lbv[a % NU]) { s->tgt[a] = lbv[a % NU]; added = 1; }
                 else if (t > ubv[a % NU]) { s->tgt[a] = ubv[a % NU]; added = 1; }

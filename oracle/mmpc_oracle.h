@@ -48,6 +48,8 @@ void oracle_set_hessian(int mode);
 /* EXACT with control bounds (projected SQP): 1 (default) = the held controls are fixed in the exact QP as in the
  * Gauss-Newton one (the kernels' bounded exact-Hessian path); 0 = bounded solves keep the Gauss-Newton Hessian */
 void oracle_set_exact_bounded(int on);
+/* control bounds: release holds whose QP multiplier points into the box (the 16-lane Riccati kernel's rule) */
+void oracle_set_bound_release(int on);
 /* W = sum_r lam[r] d^2 f_r/d(x,u)^2 of the 2-link arm (6x6 row-major, x then u; lam[4]) */
 void oracle_two_link_hess(const double* x, const double* u, const double* lam, double* W);
 

@@ -61,6 +61,7 @@ def lib():
         L.oracle_two_link_hess.argtypes = [_dp, _dp, _dp, _dp]
         L.oracle_set_hessian.argtypes = [C.c_int]
         L.oracle_set_kkt.argtypes = [C.c_int]
+        L.oracle_set_bound_release.argtypes = [C.c_int]
         L.oracle_nlp_hess.argtypes = [C.c_int, C.c_int, C.c_double, _dp, _dp, _dp, _dp, C.c_double, C.c_void_p, _dp]
         L.oracle_nlp_hess.restype = C.c_int
         _lib = L
@@ -199,17 +200,21 @@ def synth(seed, first, B, N, h, model=TWO_LINK):
 
 def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, max_iter=200,
                 tol_grad=1e-8, tol_defect=1e-10, nthreads=0, is_linear=False, model=TWO_LINK, x_lb=None, x_ub=None,
-                init_states=0, hessian=HESS_GAUSS_NEWTON, solver=None, kkt=KKT_DENSE):
+                init_states=0, hessian=HESS_GAUSS_NEWTON, solver=None, kkt=KKT_DENSE, bound_release=False):
     """solver: the GPU mmpc.Solver being checked -- the oracle then runs the Hessian that solver resolves for this
-    batch (mmpc_resolve_hessian: exact for unbounded 2-link / generated-model solves on the group kernel).
+    batch (mmpc_resolve_hessian: exact for unbounded 2-link / generated-model solves on the group kernel) and, with
+    control bounds, that kernel's active-set rule (the 16-lane Riccati kernel also releases holds whose QP multiplier
+    points into the box: bound_release).
     kkt: KKT_DENSE (default; explicit condensing) or KKT_RICCATI (the kernels' recursion; unbounded solves)."""
     if solver is not None:
         fin = lambda b: b is not None and bool((np.abs(np.asarray(b, dtype=np.float64)) < 1e19).any())  # noqa: E731
-        hessian = {1: HESS_GAUSS_NEWTON, 2: HESS_EXACT}[solver.hessian_for(int(np.asarray(x0).reshape(-1, DIMS[model][0]).shape[0]),
-                                                                          fin(u_lb) or fin(u_ub))]
+        B = int(np.asarray(x0).reshape(-1, DIMS[model][0]).shape[0])
+        hessian = {1: HESS_GAUSS_NEWTON, 2: HESS_EXACT}[solver.hessian_for(B, fin(u_lb) or fin(u_ub))]
+        bound_release = solver.kkt_solver_for(B) == 3
     lib().oracle_set_init_states(int(init_states))
     lib().oracle_set_hessian(int(hessian))
     lib().oracle_set_kkt(int(kkt))
+    lib().oracle_set_bound_release(int(bool(bound_release)))
     try:
         return _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_grad, tol_defect, nthreads,
                             is_linear, model, x_lb, x_ub)
@@ -217,6 +222,7 @@ def solve_batch(N, h, x0, u_prev, traj, weights, V=None, u_lb=None, u_ub=None, m
         lib().oracle_set_init_states(0)
         lib().oracle_set_hessian(HESS_GAUSS_NEWTON)
         lib().oracle_set_kkt(KKT_DENSE)
+        lib().oracle_set_bound_release(0)
 
 
 def _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_grad, tol_defect, nthreads,
