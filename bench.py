@@ -83,7 +83,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="cfg2 only: skip the cfg#3 / cfg#5 lines the default invocation attaches as 'secondary'")
-    ap.add_argument("--no-sweep", action="store_true", help="cfg5: skip the tolerance sweep (single tolerance)")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the tolerance sweeps (cfg5's, and cfg2's at the reference's IPOPT tol 1e-5 / "
+                                                            "SURVEY A9's 1e-6)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: --batch (default: the config's B) is the GLOBAL batch, split over the ranks "
                          "in contiguous shards (mmpc.dist.shard_strong); default: weak scaling, B per GPU")
@@ -495,6 +496,9 @@ def run_config(args, name, world, rank, primary=True):
         out["roofline"] = roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, n, iters, kern_ms, hess)
     if name == "cfg5" and world == 1 and not standin and not args.no_sweep:
         out["tolerance_sweep"] = cfg5_sweep(path, cfg, n, x0, up, tr, w, args.hessian)
+    if (name == "cfg2" and primary and world == 1 and not standin and not args.no_sweep and args.u_bound is None
+            and args.x_bound is None and args.tol is None and args.kkt == "auto" and args.hessian == "auto"):
+        out["tolerance_sweep"] = cfg5_sweep(path, cfg, n, x0, up, tr, w, args.hessian, fp32=False)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin and name != "cfg5":
         out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
                                            tol_defect, hess, None if ulb is None else args.u_bound,
@@ -507,10 +511,13 @@ def run_config(args, name, world, rank, primary=True):
     return out
 
 
-def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3):
+def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3, fp32=True):
     """SURVEY.md 8d cfg#5: the fp32-factor solve over the outer tolerance {1e-5, 1e-6, 1e-8} (tol_grad = tol,
     tol_defect = tol / 100) -- % converged, mean / max SQP iterations, kernel ms (HIP events, median of `reps`) and
-    max_i ||V_i - V_i,fp64|| / ||V_i,fp64|| against the fp64-factor solve at the default tolerances."""
+    max_i ||V_i - V_i,fp64|| / ||V_i,fp64|| against the fp64-factor solve at the default tolerances.
+    fp32=False (cfg#2): the same sweep of the fp64 solve -- what the headline kernel does at the reference's own
+    IPOPT tolerance (tol = 1e-5, ModelControl.cpp:54) and at SURVEY.md A9's build criterion (1e-6 / 1e-8), beside
+    the line's 1e-8 / 1e-10."""
     import torch
     import mmpc
 
@@ -535,15 +542,16 @@ def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3):
     Vref, st_ref, it_ref, t_ref = run(1e-8, False)
     nref = torch.linalg.vector_norm(Vref, dim=1)
     rows = []
-    for tol in (1e-5, 1e-6, 1e-8):
-        V, st, it, t = run(tol, True)
+    for tol in ((1e-5, 1e-6, 1e-8) if fp32 else (1e-5, 1e-6)):
+        V, st, it, t = run(tol, fp32)
         rel = (torch.linalg.vector_norm(V - Vref, dim=1) / nref).max().item()
-        rows.append({"factor": "fp32", "tol_grad": tol, "tol_defect": tol / 100, "converged_pct": float((st == 0).mean() * 100),
+        rows.append({"factor": "fp32" if fp32 else "fp64", "tol_grad": tol, "tol_defect": tol / 100,
+                     "converged_pct": float((st == 0).mean() * 100),
                      "mean_iters": float(it.mean()), "max_iters": int(it.max()), "kernel_ms": t,
-                     "max_rel_V_vs_fp64": rel})
+                     "solves_per_s_kernel": B / (t * 1e-3), "max_rel_V_vs_fp64": rel})
     rows.append({"factor": "fp64", "tol_grad": 1e-8, "tol_defect": 1e-10, "converged_pct": float((st_ref == 0).mean() * 100),
                  "mean_iters": float(it_ref.mean()), "max_iters": int(it_ref.max()), "kernel_ms": t_ref,
-                 "max_rel_V_vs_fp64": 0.0})
+                 "solves_per_s_kernel": B / (t_ref * 1e-3), "max_rel_V_vs_fp64": 0.0})
     return rows
 
 
