@@ -818,7 +818,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     if (j & 1) t1 = fma(arow[j], db[j], t1);
                     else t0 = fma(arow[j], db[j], t0);
                 }
-                dr = lxf * (t0 + t1);
+                // no lane-role mask on the chain: only the x-lanes' d is broadcast or stored, and the other lanes'
+                // finite leftovers (a sum of c_k[0]) are never read
+                dr = t0 + t1;
                 if (lx) sD[(k + 1) * NX + rx] = dr;
             };
             Op o0, o1;
@@ -887,7 +889,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 double lamb[NX];
                 sfor<0, NX>([&](auto I) { lamb[I] = row_bcast<I>(lamr); });
                 // (A^T lam)[r] + Q e_{k-1}[r], two partial sums
-                double t0 = lxf * (lamr + qe), t1 = 0.0;
+                // unmasked chain: a lane without an x row has Qr = 0, acol = 0 and hq = 0, so it carries 0 (XB: a finite
+                // sum of another row's z gaps) -- never broadcast or stored, and masked out of lmax
+                double t0 = lamr + qe, t1 = 0.0;
 #pragma unroll
                 for (int z = 0; z < NQ; ++z) t1 = fma(hq[z], lamb[z], t1);
 #pragma unroll
@@ -895,8 +899,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     if (s2 & 1) t1 = fma(acol[s2], lamb[NQ + s2], t1);
                     else t0 = fma(acol[s2], lamb[NQ + s2], t0);
                 }
-                lamr = lxf * (t0 + t1);
-                lmax = fmax(lmax, fabs(lamr));
+                lamr = t0 + t1;
+                lmax = fmax(lmax, fabs(lxf * lamr));
                 if (lx) sD[k * NX + rx] = lamr;
             };
             if (N >= 2) {
