@@ -35,7 +35,7 @@ namespace mmpc {
 // the Riccati step (W = P_xx A).  A field block longer than a stage simply runs on into the next stage.
 // xb: the interior-point variant's per-stage z_l, z_u, Sigma, b, z_u - z_l of (x_{k+1} | u_k) replace the hold field
 __host__ __device__ constexpr int lane_stage_stride(int nx, int nu, bool xb = false) {
-    return 5 * nx + 2 * nu + nu * (nx + nu + 1) + (xb ? 5 * (nx + nu) : nu);
+    return 5 * nx + 2 * nu + nu * (nx + nu + 1) + (xb ? 5 * (nx + nu) : 2 * nu + nx);
 }
 // linear-mode block: h-free Jacobian blocks da/dq (na x nq), da/dz (na x na), da/du (na x nu), xdot*, x*, u*
 __host__ __device__ constexpr int lane_lin_doubles(int nx, int nu, int nq) {
@@ -64,10 +64,13 @@ struct StageFields {
     static constexpr int DU = DX + NX;      // du_k
     static constexpr int K = DU + NU;       // kff_k (nu, fp64) then K_k (nu x (nx+nu), factor type)
     static constexpr int HOLD = K + NU * (NS + 1);  // bounded solves: bound u_k is held at, NaN = free
+    // unbounded solves: the second iterate buffer (x_k, u_k) -- the step sweep writes the full-step point there and an
+    // accepted full step swaps the buffers instead of running the update pass (sqp_lane_kernel SWAP)
+    static constexpr int X1 = HOLD + NU, U1 = X1 + NX;
     // interior point (XB, no hold field): y = (x_{k+1} | u_k) duals, Sigma, b, z_u - z_l
     static constexpr int NY = NX + NU;
     static constexpr int ZL = HOLD, ZU = ZL + NY, SG = ZU + NY, BB = SG + NY, ZG = BB + NY;
-    static constexpr int SS = XB ? ZG + NY : HOLD + NU;
+    static constexpr int SS = XB ? ZG + NY : U1 + NU;
     static_assert(SS == lane_stage_stride(NX, NU, XB), "layout");
 };
 
@@ -181,6 +184,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     constexpr bool WLDS = lane_w_in_lds(NX, NU, NQ);  // W's a-rows in the dead P~ slots, no HBM scratch
 #define ST(k, f, e) wsb[((int64_t)(k) * SS + (f) + (e)) * 64 + lane]  // one-off accesses
 #define SK(dk, f, e) sk[((dk) * SS + (f) + (e)) * 64]                   // stage k + dk inside a stage loop
+    // SWAP (unbounded): the iterate (x_k, u_k) lives in one of two field pairs; FX/FU name the current one, FXo/FUo
+    // the other, which the step sweep fills with the full-step point (x_k + dx_k, u_k + du_k) -- an accepted full step
+    // (99.7 % of the cfg#3 iterations) swaps the names instead of running the update pass over the workspace
+    constexpr bool SWAP = !BOUNDED && !XB;
+    int FX = SF::X, FU = SF::U, FXo = SWAP ? SF::X1 : SF::X, FUo = SWAP ? SF::U1 : SF::U;
 
     const double* w = p.weights + inst * p.w_stride;
     double Q[NX], R[NU], Rm[NU], up[NU];
@@ -200,16 +208,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int k = 0; k < N; ++k) {
 #pragma unroll
             for (int r = 0; r < NX; ++r)
-                ST(k, SF::X, r) = (k == 0 || p.init_hold) ? p.x0[inst * NX + r] : (p.init_zero ? 0.0 : Vin[k * ND + r]);
+                ST(k, FX, r) = (k == 0 || p.init_hold) ? p.x0[inst * NX + r] : (p.init_zero ? 0.0 : Vin[k * ND + r]);
 #pragma unroll
             for (int c = 0; c < NU; ++c) {
                 const double v = p.init_zero ? 0.0 : Vin[k * ND + NX + c];
-                ST(k, SF::U, c) = BOUNDED ? proj(v, lbv[c], ubv[c]) : v;
+                ST(k, FU, c) = BOUNDED ? proj(v, lbv[c], ubv[c]) : v;
             }
         }
 #pragma unroll
         for (int r = 0; r < NX; ++r)
-            ST(N, SF::X, r) = p.init_hold ? p.x0[inst * NX + r] : (p.init_zero ? 0.0 : Vin[N * ND + r]);
+            ST(N, FX, r) = p.init_hold ? p.x0[inst * NX + r] : (p.init_zero ? 0.0 : Vin[N * ND + r]);
+        if constexpr (SWAP) {   // x_0 (pinned) in both iterate buffers: the step sweep writes stages 1..N of the other
+#pragma unroll
+            for (int r = 0; r < NX; ++r) ST(0, FXo, r) = p.x0[inst * NX + r];
+        }
         const double* tr = p.traj + inst * (int64_t)N * NX;
         for (int k = 0; k < N; ++k)
 #pragma unroll
@@ -222,7 +234,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int k = 0; k < N; ++k) {
 #pragma unroll
             for (int j = 0; j < NY; ++j) {
-                double& y = j < NX ? ST(k + 1, SF::X, j) : ST(k, SF::U, j - NX);
+                double& y = j < NX ? ST(k + 1, FX, j) : ST(k, FU, j - NX);
                 y = ip_push(y, yl[j], yu[j]);
                 ST(k, SF::ZL, j) = yl[j] > -INFINITY ? 1.0 : 0.0;
                 ST(k, SF::ZU, j) = yu[j] < INFINITY ? 1.0 : 0.0;
@@ -237,7 +249,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     if (lin) {
         double x[NX], acc[NA], Fq[SQ], Fqd[NA * NA], Fu[NA * NU];
 #pragma unroll
-        for (int r = 0; r < NX; ++r) x[r] = ST(0, SF::X, r);
+        for (int r = 0; r < NX; ++r) x[r] = ST(0, FX, r);
         Model::eval_acc_jac(x, up, acc, Fq, Fqd, Fu);
 #pragma unroll
         for (int t = 0; t < NA * NQ; ++t) ST(N + 1, LFQ, t) = Fq[t];
@@ -333,12 +345,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
             for (int r = 0; r < NX; ++r) {
                 d[r] = 0.0;
-                xk[r] = ST(0, SF::X, r);
+                xk[r] = ST(0, FX, r);
             }
 #pragma unroll
             for (int c = 0; c < NU; ++c) {
                 um[c] = up[c];
-                un[c] = ST(0, SF::U, c);
+                un[c] = ST(0, FU, c);
             }
             #pragma unroll 1
             for (int k = 0; k < N; ++k) {
@@ -347,11 +359,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
                     u[c] = un[c];
-                    un[c] = SK(1, SF::U, c);  // stage N's U slot exists (unused) when k = N-1
+                    un[c] = SK(1, FU, c);  // stage N's U slot exists (unused) when k = N-1
                 }
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
-                    xn[r] = SK(1, SF::X, r);
+                    xn[r] = SK(1, FX, r);
                     rk[r] = SK(0, SF::R, r);
                 }
                 STAGE_EVAL(xk, u, xd, hFq, hFqd, hFu, true);
@@ -422,7 +434,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 }
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
-                    const double eb = ST(N, SF::X, r) - ST(N - 1, SF::R, r);  // x_N - r_{N-1}
+                    const double eb = ST(N, FX, r) - ST(N - 1, SF::R, r);  // x_N - r_{N-1}
                     pv[r] = Q[r] * eb;
                     lam[r] = Q[r] * (ST(N, SF::D, r) + eb);  // lam_N = Q e_{N-1}
                     if constexpr (XB) {  // barrier at x_N
@@ -438,10 +450,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
                     unext[c] = 0.0;
-                    upf[c] = ST(N - 1, SF::U, c);
+                    upf[c] = ST(N - 1, FU, c);
                 }
 #pragma unroll
-                for (int r = 0; r < NX; ++r) xpf[r] = ST(N - 1, SF::X, r);
+                for (int r = 0; r < NX; ++r) xpf[r] = ST(N - 1, FX, r);
                 #pragma unroll 1
                 for (int k = N - 1; k >= 0; --k) {
                     gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
@@ -459,10 +471,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                         for (int r = 0; r < NX; ++r) {
                             rkm[r] = SK(-1, SF::R, r);
-                            xpf[r] = SK(-1, SF::X, r);
+                            xpf[r] = SK(-1, FX, r);
                         }
 #pragma unroll
-                        for (int c = 0; c < NU; ++c) um[c] = SK(-1, SF::U, c);
+                        for (int c = 0; c < NU; ++c) um[c] = SK(-1, FU, c);
                     } else {
 #pragma unroll
                         for (int r = 0; r < NX; ++r) rkm[r] = 0.0;
@@ -844,12 +856,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 double xpf[NX], upf[NU], umt[NU], dt[NX];  // dt: d of the alpha = 1 trial point (FUSE_FWD)
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
-                    xpf[r] = ST(0, SF::X, r);
+                    xpf[r] = ST(0, FX, r);
                     dt[r] = 0.0;
                 }
 #pragma unroll
                 for (int c = 0; c < NU; ++c) {
-                    upf[c] = ST(0, SF::U, c);
+                    upf[c] = ST(0, FU, c);
                     umt[c] = up[c];
                 }
                 #pragma unroll 1
@@ -861,14 +873,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         x[r] = xpf[r];
-                        xpf[r] = SK(1, SF::X, r);
+                        xpf[r] = SK(1, FX, r);
                         rk[r] = SK(0, SF::R, r);
                         ck[r] = SK(0, SF::C, r);
                     }
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
                         u[c] = upf[c];
-                        upf[c] = SK(1, SF::U, c);  // stage N's U slot exists (unused) when k = N-1
+                        upf[c] = SK(1, FU, c);  // stage N's U slot exists (unused) when k = N-1
                     }
                     double du[NU];
                     const gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
@@ -959,7 +971,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                             for (int r = 0; r < NX; ++r) {
                                 const double F = fma(h, xdt[r], xt[r]);
-                                const double c = F - (xpf[r] + dx[r]);
+                                const double xn1 = xpf[r] + dx[r];   // x_{k+1} + dx_{k+1}: the update's fma(1, dx, x)
+                                if constexpr (SWAP) SK(1, FXo, r) = xn1;
+                                const double c = F - xn1;
                                 SK(0, SF::C, r) = c;
                                 cmt1 = fmax(cmt1, fabs(c));
                                 ct1 += fabs(c);
@@ -977,7 +991,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                                 const double F = fma(h, xdt[r], xt[r]);
                                 const double er = F - rk[r];
                                 Jt1 = fma(er * Q[r], er, Jt1);
-                                ct1 += fabs(F - (xpf[r] + dx[r]));
+                                const double xn1 = xpf[r] + dx[r];
+                                if constexpr (SWAP) SK(1, FXo, r) = xn1;
+                                ct1 += fabs(F - xn1);
                             }
                         }
 #pragma unroll
@@ -985,6 +1001,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                             const double dif = ut[c] - umt[c];
                             Jt1 = fma(dif * R[c], dif, fma(ut[c] * Rm[c], ut[c], Jt1));
                             umt[c] = ut[c];
+                            if constexpr (SWAP) SK(0, FUo, c) = ut[c];
                         }
                     }
                     if constexpr (XB) {  // fraction to the boundary of (x_{k+1} | u_k), barrier directional derivative
@@ -1015,11 +1032,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 ct = ct1;
             } else {
 #pragma unroll
-            for (int r = 0; r < NX; ++r) xk[r] = ST(0, SF::X, r);  // dx_0 = 0
+            for (int r = 0; r < NX; ++r) xk[r] = ST(0, FX, r);  // dx_0 = 0
 #pragma unroll
             for (int c = 0; c < NU; ++c) {
                 umt[c] = up[c];
-                upf[c] = ST(0, SF::U, c);
+                upf[c] = ST(0, FU, c);
                 dupf[c] = ST(0, SF::DU, c);
             }
             #pragma unroll 1
@@ -1030,12 +1047,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 for (int c = 0; c < NU; ++c) {
                     u[c] = fma(alpha, dupf[c], upf[c]);
                     if (BOUNDED) u[c] = proj(u[c], lbv[c], ubv[c]);  // projected trial point
-                    upf[c] = SK(1, SF::U, c);   // software pipeline as in (1)
+                    upf[c] = SK(1, FU, c);   // software pipeline as in (1)
                     dupf[c] = SK(1, SF::DU, c);
                 }
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
-                    xn[r] = fma(alpha, SK(1, SF::DX, r), SK(1, SF::X, r));
+                    xn[r] = fma(alpha, SK(1, SF::DX, r), SK(1, FX, r));
                     rk[r] = SK(0, SF::R, r);
                 }
                 {
@@ -1095,7 +1112,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
 #pragma unroll
                 for (int j = 0; j < NY; ++j) {
-                    gmem<double>& y = j < NX ? SK(1, SF::X, j) : SK(0, SF::U, j - NX);
+                    gmem<double>& y = j < NX ? SK(1, FX, j) : SK(0, FU, j - NX);
                     const double dy = j < NX ? SK(1, SF::DX, j) : SK(0, SF::DU, j - NX);
                     double zl = SK(0, SF::ZL, j), zu = SK(0, SF::ZU, j), yn;
                     ip_update(y, dy, yl[j], yu[j], zl, zu, mub, alpha, az, yn);
@@ -1105,19 +1122,40 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 }
             }
             mub = mub_next;
+        } else if constexpr (SWAP) {
+            // the other buffer holds the full-step point; after a shorter step it gets fma(alpha, d, v) instead
+            if (alpha != 1.0) {
+                #pragma unroll 1
+                for (int k = 0; k <= N; ++k) {
+                    gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
+                    if (k > 0) {
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) SK(0, FXo, r) = fma(alpha, SK(0, SF::DX, r), SK(0, FX, r));
+                    }
+                    if (k < N) {
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) SK(0, FUo, c) = fma(alpha, SK(0, SF::DU, c), SK(0, FU, c));
+                    }
+                }
+            }
+            const int tx = FX, tu = FU;
+            FX = FXo;
+            FU = FUo;
+            FXo = tx;
+            FUo = tu;
         } else {
             #pragma unroll 1
             for (int k = 0; k <= N; ++k) {
                 gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
                 if (k > 0) {
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) SK(0, SF::X, r) = fma(alpha, SK(0, SF::DX, r), SK(0, SF::X, r));
+                    for (int r = 0; r < NX; ++r) SK(0, FX, r) = fma(alpha, SK(0, SF::DX, r), SK(0, FX, r));
                 }
                 if (k < N) {
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
-                        const double un = fma(alpha, SK(0, SF::DU, c), SK(0, SF::U, c));
-                        SK(0, SF::U, c) = BOUNDED ? proj(un, lbv[c], ubv[c]) : un;
+                        const double un = fma(alpha, SK(0, SF::DU, c), SK(0, FU, c));
+                        SK(0, FU, c) = BOUNDED ? proj(un, lbv[c], ubv[c]) : un;
                     }
                 }
             }
@@ -1129,15 +1167,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     double* Vout = p.V + inst * (int64_t)NV;
     for (int k = 0; k < N; ++k) {
 #pragma unroll
-        for (int r = 0; r < NX; ++r) Vout[k * ND + r] = ST(k, SF::X, r);
+        for (int r = 0; r < NX; ++r) Vout[k * ND + r] = ST(k, FX, r);
 #pragma unroll
-        for (int c = 0; c < NU; ++c) Vout[k * ND + NX + c] = ST(k, SF::U, c);
+        for (int c = 0; c < NU; ++c) Vout[k * ND + NX + c] = ST(k, FU, c);
     }
 #pragma unroll
-    for (int r = 0; r < NX; ++r) Vout[N * ND + r] = ST(N, SF::X, r);
+    for (int r = 0; r < NX; ++r) Vout[N * ND + r] = ST(N, FX, r);
     if (p.u0_out) {
 #pragma unroll
-        for (int c = 0; c < NU; ++c) p.u0_out[inst * NU + c] = ST(0, SF::U, c);
+        for (int c = 0; c < NU; ++c) p.u0_out[inst * NU + c] = ST(0, FU, c);
     }
     if (p.status) p.status[inst] = status;
     if (p.iters) p.iters[inst] = it;
