@@ -83,7 +83,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="cfg2 only: skip the cfg#3 / cfg#5 lines the default invocation attaches as 'secondary'")
-    ap.add_argument("--no-sweep", action="store_true", help="skip the tolerance sweeps (cfg5's, and cfg2's at the reference's IPOPT tol 1e-5 / "
+    ap.add_argument("--no-sweep", action="store_true", help="skip the tolerance sweeps (cfg5's, and cfg2's / cfg3's at the reference's IPOPT tol 1e-5 / "
                                                             "SURVEY A9's 1e-6)")
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling: --batch (default: the config's B) is the GLOBAL batch, split over the ranks "
@@ -390,27 +390,27 @@ def run_config(args, name, world, rank, primary=True):
         results_to_host(k, args.warmup - 1)
     sync = (lambda: torch.cuda.synchronize(dev)) if not standin else (lambda: None)
     sync()
-    ev = ([(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-          if not standin else None)
+    # The kernel's own duration (roofline): one pair of HIP events on the launch stream around the K back-to-back
+    # launches of the timed region, / K.  No markers between launches: an event record between two launches adds a
+    # queue gap of ~6-10 us per step, while back-to-back launches run with none (rocprofv3 kernel trace,
+    # profiles/r03/gaps/), so the bracket / K is the average launch duration.
+    ev = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if not standin else None)
     if world > 1:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
+    if ev:
+        ev[0].record(stream)
     for k in range(args.steps):
-        if ev:
-            if zero_v:
-                V.zero_()
-            ev[k][0].record(stream)
-            launch(k, args.steps - 1)
-            ev[k][1].record(stream)
-        else:
-            solve(k, args.steps - 1)
+        solve(k, args.steps - 1)
+        if ev and k == args.steps - 1:
+            ev[1].record(stream)   # after the last launch (N > 1: before its result gather)
         results_to_host(k, args.steps - 1)
     sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev])) if ev else 0.0
+    kern_ms = ev[0].elapsed_time(ev[1]) / args.steps if ev else 0.0
     elapsed = mdist.max_over_ranks(elapsed, device=dev)
 
     def hbytes(k):
@@ -499,6 +499,11 @@ def run_config(args, name, world, rank, primary=True):
     if (name == "cfg2" and primary and world == 1 and not standin and not args.no_sweep and args.u_bound is None
             and args.x_bound is None and args.tol is None and args.kkt == "auto" and args.hessian == "auto"):
         out["tolerance_sweep"] = cfg5_sweep(path, cfg, n, x0, up, tr, w, args.hessian, fp32=False)
+    if (name == "cfg3" and world == 1 and not standin and not args.no_sweep and args.tol is None
+            and (not primary or (args.u_bound is None and args.x_bound is None and args.kkt == "auto"
+                                 and args.hessian == "auto"))):
+        # the exo solve at the reference's IPOPT tolerance (ModelControl.cpp:54) beside the line's 1e-8 / 1e-10
+        out["tolerance_sweep"] = cfg5_sweep(path, cfg, n, x0, up, tr, w, "auto", fp32=False)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin and name != "cfg5":
         out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
                                            tol_defect, hess, None if ulb is None else args.u_bound,
@@ -515,7 +520,7 @@ def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3, fp32=True):
     """SURVEY.md 8d cfg#5: the fp32-factor solve over the outer tolerance {1e-5, 1e-6, 1e-8} (tol_grad = tol,
     tol_defect = tol / 100) -- % converged, mean / max SQP iterations, kernel ms (HIP events, median of `reps`) and
     max_i ||V_i - V_i,fp64|| / ||V_i,fp64|| against the fp64-factor solve at the default tolerances.
-    fp32=False (cfg#2): the same sweep of the fp64 solve -- what the headline kernel does at the reference's own
+    fp32=False (cfg#2, cfg#3): the same sweep of the fp64 solve -- what the kernel does at the reference's own
     IPOPT tolerance (tol = 1e-5, ModelControl.cpp:54) and at SURVEY.md A9's build criterion (1e-6 / 1e-8), beside
     the line's 1e-8 / 1e-10."""
     import torch
