@@ -560,6 +560,36 @@ def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=3, fp32=True):
     return rows
 
 
+def model_flops_per_iteration(mmpc, cfg, ksolver, N, hess):
+    """Model-evaluation flops of one SQP iteration (full step accepted), reported beside the kernel's own KKT-algebra
+    count as SURVEY.md 8(d) asks ("Dynamics/Jacobian evaluation flops ... reported separately"): per-evaluation costs
+    from the compiled gfx950 code (mahi-mpc_amd/mmpc/model_flops.json, tools/model_flops.py; sin and cos one op each)
+    x the evaluations per stage the kernel runs per iteration:
+      16-lane kernel (sqp_group.h): the alpha = 1 trial with its Jacobian (phase A's data for the next iteration), and
+        with the exact Hessian the stage Hessian W_k;
+      lane kernel (sqp_lane.h), fp64 factor: Jacobians in the backward sweep, at (x_k, u_k) in the step sweep and at
+        the full-step point (the next forward pass); fp32 factor: forward, backward and step Jacobians + the value-only
+        alpha = 1 trial.
+    The first iteration's initial evaluation and any alpha < 1 trial are not counted (a lower bound)."""
+    try:
+        tab = json.load(open(os.path.join(os.path.dirname(mmpc.__file__), "model_flops.json")))["models"]
+    except (OSError, ValueError, KeyError):
+        return None
+    model = tab.get("ExoArm" if cfg["model"] == "exo_arm" else "TwoLinkArm")
+    if model is None:
+        return None
+    if ksolver == 3:
+        ev = {"acc_jac": 1, "hess": 1 if hess == mmpc.HESSIAN_EXACT else 0}
+    elif ksolver == 2:
+        ev = {"acc_jac": 3, "eval": 1} if cfg["fp32"] else {"acc_jac": 3}
+    else:
+        return None
+    ev = {k: v for k, v in ev.items() if v}
+    if any(k not in model for k in ev):
+        return None
+    return {"total": N * sum(n * model[k]["flops"] for k, n in ev.items()), "evals_per_stage": ev}
+
+
 def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms, hess):
     """FP64-VALU roofline of the solve kernel (the only kernel of a step besides a memset and the result pack).
 
@@ -601,6 +631,7 @@ def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_m
         except (OSError, ValueError):
             traffic = None
     alg_bytes = B * (8 * (nx + nu + N * nx + 2 * (nx * (N + 1) + nu * N)) + 12)   # SURVEY.md 8d, per launch
+    mflops = model_flops_per_iteration(mmpc, cfg, ksolver, N, hess)
     return {"bound": "fp64-valu", "achieved": own, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": own / FP64_PEAK_TFLOPS, "traffic": traffic,
             "traffic_source": traffic_src,
@@ -611,6 +642,12 @@ def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_m
             "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N, nx, nu),
             "survey_8d_equivalent_tflops": survey,
             "survey_8d_equivalent_frac": survey / FP64_PEAK_TFLOPS,
+            "model_eval_flops_per_iter": mflops and mflops["total"],
+            "model_evals_per_stage_iter": mflops and mflops["evals_per_stage"],
+            "achieved_incl_model_evals": (float(iters.sum()) * (fl["total"] + mflops["total"]) / sec / 1e12
+                                          if mflops else None),
+            "frac_incl_model_evals": (float(iters.sum()) * (fl["total"] + mflops["total"]) / sec / 1e12
+                                      / FP64_PEAK_TFLOPS if mflops else None),
             "algorithmic_hbm_bytes_per_launch": alg_bytes,
             "hbm_gbs_algorithmic": alg_bytes / sec / 1e9,
             "pmc_fp64_valu_flops_issued_per_launch": pmc.get("fp64_valu_flops_issued_per_launch"),
@@ -621,7 +658,8 @@ def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_m
             "pmc_valu_active_frac": pmc.get("valu_active_frac"),
             "note": "frac = the kernel's own algorithmic flops / FP64 vector peak (no kernel issues MFMA: DESIGN.md "
                     "'Why no MFMA'); pmc_* = rocprofv3 counters (tools/pmc.sh) of the same kernel, shape and library "
-                    "build (lib_sha256): issued FP64 VALU lane-flops incl. inactive-lane slots"}
+                    "build (lib_sha256): issued FP64 VALU lane-flops incl. inactive-lane slots; *_incl_model_evals add "
+                    "the model / Jacobian / Hessian evaluation flops (model_eval_flops_per_iter, SURVEY.md 8(d))"}
 
 
 def main():

@@ -56,3 +56,18 @@ def test_launcher_strong_scaling_ragged(gpus):
     assert out["scaling"] == "strong" and out["config"]["global_batch"] == 10
     assert out["gathered_results_match"] is True and out["converged"] == 10
     assert out["standin_u0_first_col"] == [float(i) for i in range(10)]
+
+
+def test_model_eval_flops_table():
+    """bench.py's roofline reports the model-evaluation flops beside the KKT algebra; the table
+    comes from the compiled gfx950 code (tools/model_flops.py) and covers every evaluation the default lines use."""
+    import bench
+    import mmpc
+    g = bench.model_flops_per_iteration(mmpc, bench.CONFIGS["cfg2"], 3, 30, mmpc.HESSIAN_EXACT)
+    assert g["evals_per_stage"] == {"acc_jac": 1, "hess": 1} and 5_000 < g["total"] < 50_000
+    gn = bench.model_flops_per_iteration(mmpc, bench.CONFIGS["cfg2"], 3, 30, mmpc.HESSIAN_GAUSS_NEWTON)
+    assert gn["evals_per_stage"] == {"acc_jac": 1} and gn["total"] < g["total"]
+    e = bench.model_flops_per_iteration(mmpc, bench.CONFIGS["cfg3"], 2, 50, mmpc.HESSIAN_GAUSS_NEWTON)
+    f = bench.model_flops_per_iteration(mmpc, bench.CONFIGS["cfg5"], 2, 50, mmpc.HESSIAN_GAUSS_NEWTON)
+    assert e["evals_per_stage"] == {"acc_jac": 3} and f["total"] > e["total"] > 50_000
+    assert bench.model_flops_per_iteration(mmpc, bench.CONFIGS["cfg2"], 1, 30, mmpc.HESSIAN_GAUSS_NEWTON) is None
