@@ -7,7 +7,7 @@ import collections
 import re
 import sys
 
-ASM = "mahi-mpc_amd/build/mmpc.s"
+ASM = sys.argv[2] if len(sys.argv) > 2 else "mahi-mpc_amd/build/mmpc.s"
 key = sys.argv[1] if len(sys.argv) > 1 else "sqp_group_kernelINS_10TwoLinkArmELb0ELb0"
 s = open(ASM).read()
 name = [m.group(1) for m in re.finditer(r"^(_Z\S+):", s, re.M) if key in m.group(1)][0]
