@@ -393,7 +393,8 @@ def run_config(args, name, world, rank, primary=True):
     # The kernel's own duration (roofline): one pair of HIP events on the launch stream around the K back-to-back
     # launches of the timed region, / K.  No markers between launches: an event record between two launches adds a
     # queue gap of ~6-10 us per step, while back-to-back launches run with none (rocprofv3 kernel trace,
-    # profiles/r03/gaps/), so the bracket / K is the average launch duration.
+    # profiles/r03/gaps/), so the bracket / K is the average launch duration (with --init as_given it also holds the
+    # per-step memset of V, a few microseconds).
     ev = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if not standin else None)
     if world > 1:
         dist.barrier()
