@@ -52,6 +52,8 @@ struct TwoLinkArm {
     MMPC_HD static void eval_hess(const double* x, const double* u, const double* lam, double* W) {
         TwoLinkFast::eval_hess(x, u, lam, W);
     }
+    // acc is affine in the torques (acc = M(q)^-1 (T - ...)), so the u-u block of every W is exactly zero
+    static constexpr bool kControlAffine = true;
 };
 
 // Second derivatives available (Model::eval_hess): exact-Hessian SQP and mmpc_nlp_hess_batch
@@ -61,6 +63,15 @@ struct HasHess {
 };
 template <class M>
 struct HasHess<M, std::enable_if_t<M::kHasHess>> {
+    static constexpr bool value = true;
+};
+// Dynamics affine in u (d^2 acc / du^2 == 0): the exact-Hessian sweep skips the u-u block of W_k, which is zero
+template <class M, class = void>
+struct IsControlAffine {
+    static constexpr bool value = false;
+};
+template <class M>
+struct IsControlAffine<M, std::enable_if_t<M::kControlAffine>> {
     static constexpr bool value = true;
 };
 

@@ -199,6 +199,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     //      (XB) add the barrier terms and use the Cholesky (Y^T Y) form of the stage update.  Models with
     //      nx + nu >= 16 keep the one-lane sweep below. ----
     constexpr bool DIST = (NS < G);
+    // control-affine model: the u-u block of the exact-Hessian W_k is zero -- neither stored, loaded nor added
+    constexpr bool CAFF = IsControlAffine<Model>::value;
     static_assert(!EXACT || (DIST && HasHess<Model>::value), "exact Hessian: lane-distributed path, model eval_hess");
     const int r = gl;
     const bool lx = r < NX, lu = r >= NX && r < NS, la = r >= NQ && r < NX;
@@ -952,8 +954,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             auto load_w = [&](int k, Wb& b) {
 #pragma unroll
                 for (int j = 0; j < KZ; ++j) b.r[j] = lxm * wH[k * HW + rx * KZ + j];
+                if constexpr (!CAFF) {
 #pragma unroll
-                for (int j = 0; j < NU * NU; ++j) b.u[j] = wH[k * HW + NX * KZ + j];
+                    for (int j = 0; j < NU * NU; ++j) b.u[j] = wH[k * HW + NX * KZ + j];
+                }
             };
             if (EXACT && useW) {
                 load_w(N - 1, w0);
@@ -998,7 +1002,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                     for (int j = 0; j < KZ; ++j) wr[j] = useW ? wb.r[j] : 0.0;
 #pragma unroll
-                    for (int j = 0; j < NU * NU; ++j) wu[j] = useW ? wb.u[j] : 0.0;
+                    for (int j = 0; j < NU * NU; ++j) wu[j] = (useW && !CAFF) ? wb.u[j] : 0.0;
                     if (!LAST && useW) load_w(k >= 2 ? k - 2 : 0, wb);   // k = 1: a harmless reload of stage 0
                 }
                 // T = P~ [B; I] (row r), mv = P~_x. c + p~ (row r)
@@ -1028,7 +1032,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                         for (int s2 = 0; s2 < NA; ++s2) t = fma(hFu[s2 * NU + a], Tb[NQ + s2][b], t);
                         if (a == b) t += R[a] + Rm[a];
-                        if constexpr (EXACT) t += wu[a * NU + b];
+                        if constexpr (EXACT && !CAFF) t += wu[a * NU + b];
                         if constexpr (XB) {
                             if (a == b) t += sSg[k * NY + NX + a];   // barrier Sigma of u_k
                         }
@@ -1406,10 +1410,12 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 for (int r2 = 0; r2 < NX; ++r2)
 #pragma unroll
                     for (int j = 0; j < KZ; ++j) dst[r2 * KZ + j] = W[r2 * KZ + j];
+                if constexpr (!CAFF) {
 #pragma unroll
-                for (int a = 0; a < NU; ++a)
+                    for (int a = 0; a < NU; ++a)
 #pragma unroll
-                    for (int b = 0; b < NU; ++b) dst[NX * KZ + a * NU + b] = W[(NX + a) * KZ + NX + b];
+                        for (int b = 0; b < NU; ++b) dst[NX * KZ + a * NU + b] = W[(NX + a) * KZ + NX + b];
+                }
             }
             // the stores of the other lanes of this wave must be visible to the sweep's loads
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
