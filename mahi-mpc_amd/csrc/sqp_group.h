@@ -944,13 +944,13 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         auto backward_dist = [&](bool useW) {
             double Prow[NS], pvr;
             const double lxm = lx ? 1.0 : 0.0;
-            // W_k row rx and uu block from the workspace, prefetched TWO stages ahead into alternating buffers
-            // (stage k reads buffer (N-1-k) & 1; one stage of distance left the load of W_{k-1}, an L2/MALL round
-            // trip, exposed at the top of every stage)
+            // W_k row rx and uu block from the workspace, loaded one stage ahead into one buffer.  (Round 2 used two
+            // buffers two stages ahead; once the control-affine sweep dropped the uu block, the second buffer's
+            // registers cost more than the load latency it hid: 0.1875 -> 0.1808 ms with one buffer)
             struct Wb {
                 double r[KZ], u[NU * NU];
             };
-            Wb w0, w1;
+            Wb w0;
             auto load_w = [&](int k, Wb& b) {
 #pragma unroll
                 for (int j = 0; j < KZ; ++j) b.r[j] = lxm * wH[k * HW + rx * KZ + j];
@@ -961,7 +961,6 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             };
             if (EXACT && useW) {
                 load_w(N - 1, w0);
-                load_w(N >= 2 ? N - 2 : 0, w1);
             }
 #pragma unroll
             for (int j = 0; j < NS; ++j) Prow[j] = j < NX ? qoh[j] : 0.0;   // P~_N = blkdiag(Q, 0)
@@ -1003,7 +1002,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     for (int j = 0; j < KZ; ++j) wr[j] = useW ? wb.r[j] : 0.0;
 #pragma unroll
                     for (int j = 0; j < NU * NU; ++j) wu[j] = (useW && !CAFF) ? wb.u[j] : 0.0;
-                    if (!LAST && useW) load_w(k >= 2 ? k - 2 : 0, wb);   // k = 1: a harmless reload of stage 0
+                    if (!LAST && useW) load_w(k - 1, wb);
                 }
                 // T = P~ [B; I] (row r), mv = P~_x. c + p~ (row r)
                 double T[NU], mv = pvr;
@@ -1303,14 +1302,14 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             if ((N - 1) & 1) {
                 stage(N - 1, F_{}, w0);
                 for (int k = N - 2; k >= 2; k -= 2) {
-                    stage(k, F_{}, w1);
+                    stage(k, F_{}, w0);
                     stage(k - 1, F_{}, w0);
                 }
-                stage(0, std::true_type{}, w1);
+                stage(0, std::true_type{}, w0);
             } else {
                 for (int k = N - 1; k >= 2; k -= 2) {
                     stage(k, F_{}, w0);
-                    stage(k - 1, F_{}, w1);
+                    stage(k - 1, F_{}, w0);
                 }
                 stage(0, std::true_type{}, w0);
             }
