@@ -953,7 +953,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             Wb w0;
             auto load_w = [&](int k, Wb& b) {
 #pragma unroll
-                for (int j = 0; j < KZ; ++j) b.r[j] = lxm * wH[k * HW + rx * KZ + j];
+                for (int j = 0; j < KZ; ++j) b.r[j] = wH[k * HW + rx * KZ + j];   // row rx; masked at its uses
                 if constexpr (!CAFF) {
 #pragma unroll
                     for (int j = 0; j < NU * NU; ++j) b.u[j] = wH[k * HW + NX * KZ + j];
@@ -1052,7 +1052,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                     for (int q = 0; q < NX; ++q) tb[q] = Tb[q][a];
                     Ycol[a] = colA(T[a], acol, tb) - rdg[a];
-                    if constexpr (EXACT) Ycol[a] += wr[NX + a];   // H_wx[a][r] += W_ux[a][r] (x-lanes; 0 else)
+                    if constexpr (EXACT) Ycol[a] = fma(lxm, wr[NX + a], Ycol[a]);   // H_wx[a][r] += W_ux[a][r] (x-lanes)
                 }
                 // BOUNDED: the un-held stage rows [H_wx | -R | H_ww | h_w] (lane j < NS: column j; lanes NS.. the H_ww
                 // columns and h_w, the idle lanes duplicating h_w) -- the step sweep forms the multiplier of a held
@@ -1285,7 +1285,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 for (int j = 0; j < NS; ++j) {
                     double v = j < NX ? Pn[j] + qoh[j] : rdg[j - NX];
                     if constexpr (EXACT) {
-                        if (j < NX) v += wr[j];   // W_xx row r
+                        if (j < NX) v = fma(lxm, wr[j], v);   // W_xx row r (x-lanes; the mask folded into the add)
                     }
 #pragma unroll
                     for (int a = 0; a < NU; ++a) v = fma(-Ycol[a], j < NX ? Kb[a][j] : Ku[a][j - NX], v);
