@@ -812,7 +812,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                 for (int s2 = 0; s2 < NA; ++s2) arow[NQ + s2] = fma(lad, o.d[s2], hrow[NQ + s2]);
                 const double cr = o.c;
-                fetch(k + 2 < N ? k + 2 : N - 1, o);   // unconditional: static wait counts
+                // unconditional and unclamped (static wait counts; the address is a strength-reduced increment): past
+                // the last stage the loads read the next arrays of this instance's LDS block (sFq -> sFqd -> sFu,
+                // sC -> sFq), values never used
+                fetch(k + 2, o);
                 sfor<0, NX>([&](auto I) { db[I] = row_bcast<I>(dr); });
                 double t0 = dr + cr, t1 = 0.0;
 #pragma unroll
@@ -993,7 +996,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 double exr = 0.0, duu = 0.0;
                 if constexpr (!LAST) {
                     const double xk = sX[k * NX + rx], trm = tr[(k - 1) * NX + rx];
-                    exr = lx ? xk - trm : 0.0;
+                    exr = xk - trm;   // non-x lanes: finite leftovers of the clamped row, masked by lxm in pn
                     duu = sU[k * NU + ru] - sU[(k - 1) * NU + ru];
                 }
                 double wr[KZ], wu[NU * NU];
