@@ -101,6 +101,10 @@ def parse(argv=None):
                     help="mmpc_opts.hessian: AUTO = exact Lagrangian Hessian where supported (DESIGN.md 3e)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic_latest.json"),
                     help="PMC-derived HBM bytes per launch per config (tools/pmc.sh + tools/pmc_summary.py)")
+    ap.add_argument("--rccl", action="store_true",
+                    help="N = 1 too: initialise the RCCL process group (\"nccl\") and gather the last step's result "
+                         "table through all_gather_into_tensor as the N > 1 path does, so the RCCL leg runs on a "
+                         "one-GPU box (the line then reports the RCCL version)")
     ap.add_argument("--standin", action="store_true",
                     help="TEST ONLY: CPU tensors, gloo and a trivial stand-in solver, to exercise the launcher / "
                          "rank / gather plumbing without a GPU (tests/test_bench_launch.py); never a measurement")
@@ -252,11 +256,26 @@ def run_rank(args):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world > 1:
+    pg = world > 1 or args.rccl
+    if pg:
         # MMPC_BENCH_BACKEND / MMPC_BENCH_SAME_DEVICE: test hooks that rehearse the N > 1 GPU path on a one-GPU box
         # (gloo ranks sharing device 0; RCCL rejects two ranks on one GPU) -- never set for measurements
+        if world == 1:   # --rccl at N = 1: a one-rank group (legal on one GPU), not launched by torchrun
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if args.rccl:
+            import mmpc.dist as mdist
+            mdist.force_collectives(True)
+        if not args.standin:   # RCCL binds the communicator to the current device
+            import torch
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) if not os.environ.get("MMPC_BENCH_SAME_DEVICE") else 0)
         dist.init_process_group(os.environ.get("MMPC_BENCH_BACKEND") or ("gloo" if args.standin else "nccl"))
     out = run_config(args, args.config, world, rank, primary=True)
+    if pg:
+        import mmpc.dist as mdist
+        out["process_group"] = mdist.rccl_info()
     # the default (headline) invocation also measures the exo workloads of SURVEY.md 8d inside the same run, so the
     # driver's clock covers them: cfg#3 (at N > 1 ranks: cfg#4, weak-scaled 65536 instances per GPU) and cfg#5
     if args.config == "cfg2" and not args.no_secondary and not args.standin and args.batch is None \
@@ -264,7 +283,7 @@ def run_rank(args):
         out["secondary"] = {c: run_config(args, c, world, rank, primary=False) for c in ("cfg3", "cfg5")}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 
@@ -282,6 +301,9 @@ def run_config(args, name, world, rank, primary=True):
     # rows of this rank: weak scaling -- B per rank, global instances [r B, (r+1) B); strong -- the global batch B split
     # in contiguous shards; Bc = result-table rows per rank (equal for the gather; strong shards may be ragged)
     strong = args.strong and primary
+    coll = world > 1 or args.rccl   # the last step's result table goes through the collective gather
+    if strong and B < world:
+        raise SystemExit(f"--strong needs --batch >= the rank count ({B} < {world}): a rank would get no instances")
     Bt = B if strong else B * world
     Bc = -(-B // world) if strong else B
     first, n = mdist.shard_strong(B, rank, world) if strong else mdist.shard(B, rank)
@@ -355,20 +377,20 @@ def run_config(args, name, world, rank, primary=True):
     solver.synth(SEED, first, n, x0, up, tr, stream=sh)
     mdist.broadcast_shared(w)   # shared weights from rank 0 (identical here by construction)
 
-    table = torch.empty(world * nbytes, dtype=torch.uint8, device=dev) if world > 1 else res
+    table = torch.empty(world * nbytes, dtype=torch.uint8, device=dev) if coll else res
     pin = dict(pin_memory=True) if not standin else {}
     host = [torch.empty(world * nbytes, dtype=torch.uint8, **pin) for _ in range(2)]
     # MMPC_INIT_ZERO: the cold start V = 0 without reading V (no per-step memset); as_given zeroes V each step
     zero_v = args.init == "as_given" or standin
 
     def zc(k, last):   # this step's results straight into host memory?
-        return zero_copy and (world == 1 or k != last)
+        return zero_copy and (not coll or k != last)
 
     def results_to_host(k, last):
         if zc(k, last):
             return   # stored into host memory by the solve kernel
         u0[:n].copy_(V[:, nx:nx + nu])
-        if world > 1:   # N > 1: one all_gather_into_tensor (RCCL over xGMI) to rank 0's device, then D2H there
+        if coll:   # N > 1 (or --rccl): one all_gather_into_tensor (RCCL over xGMI) to rank 0's device, then D2H there
             dist.all_gather_into_tensor(table, res, async_op=True).wait()   # stream-ordered on GPUs
         if rank == 0:
             host[k % 2].copy_(table, non_blocking=not standin)
@@ -396,7 +418,7 @@ def run_config(args, name, world, rank, primary=True):
     # profiles/r03/gaps/), so the bracket / K is the average launch duration (with --init as_given it also holds the
     # per-step memset of V, a few microseconds).
     ev = ((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if not standin else None)
-    if world > 1:
+    if coll:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
@@ -408,7 +430,7 @@ def run_config(args, name, world, rank, primary=True):
             ev[1].record(stream)   # after the last launch (N > 1: before its result gather)
         results_to_host(k, args.steps - 1)
     sync()
-    if world > 1:
+    if coll:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = ev[0].elapsed_time(ev[1]) / args.steps if ev else 0.0
@@ -420,7 +442,7 @@ def run_config(args, name, world, rank, primary=True):
     # zero-copy results check: None = unchecked (N > 1 needs two timed steps: the previous step's host buffer holds
     # the same instances as the gathered last step)
     zc_ok = None
-    if zero_copy and world == 1:   # the host buffer of the last step IS the result table; check it against V
+    if zero_copy and not coll:   # the host buffer of the last step IS the result table; check it against V
         hb = hviews[(args.steps - 1) % 2]
         res.copy_(hbytes(args.steps - 1))
         host[(args.steps - 1) % 2].copy_(res.cpu())
@@ -440,7 +462,7 @@ def run_config(args, name, world, rank, primary=True):
     else:
         conv = 0
         tail = None
-    if world > 1:
+    if coll:
         ok = bool(torch.equal(table[rank * nbytes:(rank + 1) * nbytes].cpu(), mine)) and ok
         ok = mdist.sum_over_ranks(int(not ok), device=dev if not standin else None) == 0
     total = Bt * args.steps
@@ -474,10 +496,10 @@ def run_config(args, name, world, rank, primary=True):
                    "parallelism": (f"batch-shard x{world}; per-step results (u_0*, status, iters) stored by the "
                                    "solve kernel into each rank's pinned host memory (mmpc_host_alloc); the last "
                                    "step's table gathered to rank 0 by RCCL all_gather_into_tensor + D2H"
-                                   if world > 1 else "batch-shard x1; per-step results (u_0*, status, iters) stored "
+                                   if coll else "batch-shard x1; per-step results (u_0*, status, iters) stored "
                                                      "by the solve kernel into pinned host memory (mmpc_host_alloc)"),
                    "timed_region": ("cold-start solves + per-step results (u_0*, status, iters) on the host"
-                                    + ("; the last step's table of all ranks on rank 0's host" if world > 1 else ""))},
+                                    + ("; the last step's table of all ranks on rank 0's host" if coll else ""))},
         "converged": conv,
         "gathered_results_match": ok,
         "zero_copy_results_checked": zc_ok is not None,
@@ -569,9 +591,9 @@ def model_flops_per_iteration(mmpc, cfg, ksolver, N, hess):
     x the evaluations per stage the kernel runs per iteration:
       16-lane kernel (sqp_group.h): the alpha = 1 trial with its Jacobian (phase A's data for the next iteration), and
         with the exact Hessian the stage Hessian W_k;
-      lane kernel (sqp_lane.h), fp64 factor: Jacobians in the backward sweep, at (x_k, u_k) in the step sweep and at
-        the full-step point (the next forward pass); fp32 factor: forward, backward and step Jacobians + the value-only
-        alpha = 1 trial.
+      lane kernel (sqp_lane.h; round 4: the backward and step sweeps read the stage Jacobian stored where it was
+        evaluated, models.h JacPack), fp64 factor: one Jacobian per stage, at the full-step point (the alpha = 1 trial,
+        the next iteration's A_k, B_k); fp32 factor: the forward pass's Jacobian + the value-only alpha = 1 trial.
     The first iteration's initial evaluation and any alpha < 1 trial are not counted (a lower bound)."""
     try:
         tab = json.load(open(os.path.join(os.path.dirname(mmpc.__file__), "model_flops.json")))["models"]
@@ -583,7 +605,7 @@ def model_flops_per_iteration(mmpc, cfg, ksolver, N, hess):
     if ksolver == 3:
         ev = {"acc_jac": 1, "hess": 1 if hess == mmpc.HESSIAN_EXACT else 0}
     elif ksolver == 2:
-        ev = {"acc_jac": 3, "eval": 1} if cfg["fp32"] else {"acc_jac": 3}
+        ev = {"acc_jac": 1, "eval": 1} if cfg["fp32"] else {"acc_jac": 1}
     else:
         return None
     ev = {k: v for k, v in ev.items() if v}

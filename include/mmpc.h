@@ -128,9 +128,11 @@ enum mmpc_hessian {
                                       tracking residuals */
     MMPC_HESSIAN_EXACT = 2         /* + h sum_r lam_{k+1,r} d^2 f_r/d(x_k,u_k)^2 per stage (lam: the QP adjoint);
                                       an iteration whose KKT matrix is not positive definite on the null space takes
-                                      the Gauss-Newton step.  Supported: unbounded, nonlinear solves of models with
-                                      second derivatives on the RICCATI_GROUP solver (nx+nu < 16); a solve outside
-                                      that returns MMPC_ERR_UNSUPPORTED */
+                                      the Gauss-Newton step.  Supported: nonlinear solves of models with second
+                                      derivatives on the RICCATI_GROUP solver (nx+nu < 16), unbounded or with control
+                                      bounds (the held controls are fixed in the exact QP; AUTO keeps Gauss-Newton
+                                      for bounded solves); state bounds and any other solve return
+                                      MMPC_ERR_UNSUPPORTED */
 };
 
 typedef struct mmpc_opts {
@@ -185,8 +187,9 @@ int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes);
 int mmpc_resolve_kkt_solver(const mmpc_handle* h, int64_t B, int32_t* solver);
 
 /* The Hessian (MMPC_HESSIAN_GAUSS_NEWTON or MMPC_HESSIAN_EXACT) a solve of B instances runs under the handle's
- * options; u_bounded = whether the solve passes control bounds (the projected solves are Gauss-Newton).
- * MMPC_ERR_UNSUPPORTED when opts.hessian = EXACT cannot be honoured for that solve. */
+ * options; u_bounded = whether the solve passes control bounds (AUTO resolves control-bounded solves to
+ * Gauss-Newton; an explicit EXACT is honoured with control bounds on RICCATI_GROUP).
+ * MMPC_ERR_UNSUPPORTED when opts.hessian = EXACT cannot be honoured for that solve (state bounds, other solvers). */
 int mmpc_resolve_hessian(const mmpc_handle* h, int64_t B, int32_t u_bounded, int32_t* hessian);
 
 /* Batched SQP solve, DEVICE pointers, stream-ordered.  u_lb/u_ub: device [nu] or NULL

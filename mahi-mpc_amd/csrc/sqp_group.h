@@ -30,18 +30,25 @@ constexpr int kGroupsPerWave = 4;
 // 160 KB; with them 41 KB leaves one SIMD of every CU idle (measured: 0.78 vs 0.6x ms).
 // nq = kinematic rows of the model (sqp_lane.h a_mul); the stage blocks are h da/dq, h da/dz, h da/du.
 // xb: the interior-point variant (state bounds) adds z_l, z_u, Sigma, b, z_u - z_l per stage for (x_{k+1} | u_k).
+// The d recursion prefetches two stages ahead without a clamp (d_recursion_dist): its reads of stages N and N + 1 of
+// sC, sFq and sFqd land in the arrays that follow each of them; the tail pad of 2 (nx - nq)^2 doubles keeps the last
+// one (sFqd) inside the instance's own block even when N nu < 2 (nx - nq) (exo shapes at N = 1), never in the next
+// group's block or past the end of the dynamic LDS.  The prefetched values are never used.
 __host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int nq, int N, bool bounded = true,
                                                    bool linear = true, bool xb = false) {
     return N * (3 * nx + (nx - nq) * (nq + (nx - nq) + nu) + 2 * nu) + 3 * (N + 1) * nx + (bounded ? N * nu : 0) +
-           (linear ? (nx - nq) * (nq + (nx - nq) + nu) + nx : 0) + (xb ? 5 * N * (nx + nu) : 0);
+           (linear ? (nx - nq) * (nq + (nx - nq) + nu) + nx : 0) + (xb ? 5 * N * (nx + nu) : 0) +
+           2 * (nx - nq) * (nx - nq);
 }
 // exact Hessian (EXACT): per stage the x rows of W_k = h sum_s lam_{k+1,NQ+s} d^2 acc_s/d(x,u)^2 (nx x (nx+nu))
 // and its u-u block (nu x nu), written stage-parallel and read by the lane-distributed Riccati sweep
 __host__ __device__ constexpr int group_hess_doubles(int nx, int nu) { return nx * (nx + nu) + nu * nu; }
 // HBM workspace doubles per instance: K_k | kff_k per stage, then the W_k blocks per stage, then (control-bounded
-// solves) the un-held rows [H_wx | -R | H_ww | h_w] of each stage QP, for the multipliers of the held controls
-__host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N) {
-    return N * nu * (nx + nu + 1) + N * group_hess_doubles(nx, nu) + N * nu * (nx + 2 * nu + 1);
+// solves only) the un-held rows [H_wx | -R | H_ww | h_w] of each stage QP, for the multipliers of the held controls.
+// The kernel strides instances by its own variant's size (unbounded solves: 1020 instead of 1560 doubles at cfg#2);
+// the host reserves the bounded size, the largest.
+__host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N, bool bounded = true) {
+    return N * nu * (nx + nu + 1) + N * group_hess_doubles(nx, nu) + (bounded ? N * nu * (nx + 2 * nu + 1) : 0);
 }
 
 struct GroupWork {
@@ -173,7 +180,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const sSg = sZu + N * NY;
     double* const sBb = sSg + N * NY;
     double* const sZg = sBb + N * NY;
-    double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N);  // [N][NU][NS+1]
+    double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N, BOUNDED);  // [N][NU][NS+1]
     constexpr int KZ = NX + NU, HW = group_hess_doubles(NX, NU);
     double* const wH = wK + N * NU * (NS + 1);  // EXACT: [N][HW] = W_k x rows [NX][KZ] | W_k uu block [NU][NU]
     constexpr int NR = NS + NU + 1;             // BOUNDED: [N][NU][NR] = un-held [H_wx | -R | H_ww | h_w] rows
@@ -945,6 +952,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             }
         };
         auto backward_dist = [&](bool useW) {
+            if constexpr (BOUNDED) {   // the hold targets (sHold) the gradient pass stored on every lane of this wave
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
             double Prow[NS], pvr;
             const double lxm = lx ? 1.0 : 0.0;
             // W_k row rx and uu block from the workspace, loaded one stage ahead into one buffer.  (Round 2 used two

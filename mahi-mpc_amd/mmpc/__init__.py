@@ -210,6 +210,8 @@ class HostBuffer:
         self.ptr = p.value or 0
         self.nbytes = int(nbytes)
         self._buf = (C.c_char * self.nbytes).from_address(self.ptr) if self.nbytes else None
+        if self.nbytes:   # hipHostMalloc does not zero: rows a ragged shard never writes must compare equal
+            C.memset(self.ptr, 0, self.nbytes)
 
     def view(self, offset: int, dtype, count: int) -> np.ndarray:
         dt = np.dtype(dtype)

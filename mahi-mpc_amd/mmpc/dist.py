@@ -9,6 +9,41 @@ Process group: RCCL over xGMI on GPUs ("nccl"), gloo in the CPU tests."""
 from __future__ import annotations
 
 
+# Collectives even with one rank: the helpers below skip the collective at world size 1 (nothing to exchange).
+# force_collectives(True) makes them issue it anyway, so the RCCL path (all_gather_into_tensor, broadcast, scatter)
+# can be exercised on a one-GPU box (tests/test_gpu_rccl.py, bench.py --rccl).
+_FORCE = False
+
+
+def force_collectives(flag: bool = True) -> bool:
+    """issue the collectives at world size 1 too; returns the previous setting"""
+    global _FORCE
+    prev, _FORCE = _FORCE, bool(flag)
+    return prev
+
+
+def _multi():
+    """a process group whose collectives must run: world size > 1, or forced"""
+    import torch.distributed as dist
+    return dist.is_available() and dist.is_initialized() and (dist.get_world_size() > 1 or _FORCE)
+
+
+def rccl_info():
+    """backend and, on GPUs, the RCCL version the process group runs on (None without a process group)"""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    info = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
+    if info["backend"] == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            info["rccl_version"] = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception as e:   # pragma: no cover - reported, not fatal
+            info["rccl_version"] = f"unknown ({e})"
+    return info
+
+
 def shard(batch_per_rank: int, rank: int) -> tuple[int, int]:
     """(first global instance index, count) of this rank (weak scaling: fixed work per rank)."""
     if batch_per_rank < 0 or rank < 0:
@@ -26,7 +61,7 @@ def shard_strong(total: int, rank: int, world: int) -> tuple[int, int]:
 def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _multi():
         return float(value)
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -36,7 +71,7 @@ def max_over_ranks(value: float, device=None) -> float:
 def sum_over_ranks(value, device=None):
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not _multi():
         return value
     t = torch.tensor([value], dtype=torch.float64 if isinstance(value, float) else torch.int64, device=device)
     dist.all_reduce(t)
@@ -58,7 +93,7 @@ def broadcast_shared(*tensors, src: int = 0):
     """Broadcast the shared (per-batch) solve parameters in place (weights [nx+2nu], u_lb/u_ub [nu]); None
     entries are skipped (every rank must pass the same pattern)."""
     import torch.distributed as dist
-    if _pg_ready() and dist.get_world_size() > 1:
+    if _multi():
         for t in tensors:
             if t is not None:
                 dist.broadcast(t, src=src)
@@ -71,7 +106,7 @@ def gather_rows(local, total_rows: int, dst: int = 0):
     One all_gather_into_tensor of equal-sized, padded chunks (RCCL over xGMI on GPUs, gloo on CPUs)."""
     import torch
     import torch.distributed as dist
-    if not _pg_ready() or dist.get_world_size() == 1:
+    if not _multi():
         return local
     world, rank = dist.get_world_size(), dist.get_rank()
     chunk = -(-total_rows // world)
@@ -90,7 +125,7 @@ def scatter_rows(full, total_rows: int, row_shape, dtype, device, src: int = 0):
     """Rank ``src`` holds ``full`` [total_rows, *row_shape]; every rank receives its shard_strong rows."""
     import torch
     import torch.distributed as dist
-    if not _pg_ready() or dist.get_world_size() == 1:
+    if not _multi():
         return full
     world, rank = dist.get_world_size(), dist.get_rank()
     chunk = -(-total_rows // world)
@@ -128,7 +163,7 @@ def solve_rank0_batch(solver, x0=None, u_prev=None, traj=None, weights=None, V=N
         meta[2] = int(u_lb is not None)
         meta[3] = int(u_ub is not None)
         meta[4] = int(weights_stride)
-    if world > 1:
+    if _multi():
         dist.broadcast(meta, src=0)
     B, has_V, has_lb, has_ub, ws = (int(v) for v in meta.tolist())
     f64 = dict(dtype=torch.float64, device=device)

@@ -69,5 +69,23 @@ def test_model_eval_flops_table():
     assert gn["evals_per_stage"] == {"acc_jac": 1} and gn["total"] < g["total"]
     e = bench.model_flops_per_iteration(mmpc, bench.CONFIGS["cfg3"], 2, 50, mmpc.HESSIAN_GAUSS_NEWTON)
     f = bench.model_flops_per_iteration(mmpc, bench.CONFIGS["cfg5"], 2, 50, mmpc.HESSIAN_GAUSS_NEWTON)
-    assert e["evals_per_stage"] == {"acc_jac": 3} and f["total"] > e["total"] > 50_000
+    assert e["evals_per_stage"] == {"acc_jac": 1} and f["evals_per_stage"] == {"acc_jac": 1, "eval": 1}
+    assert f["total"] > e["total"] > 50_000
     assert bench.model_flops_per_iteration(mmpc, bench.CONFIGS["cfg2"], 1, 30, mmpc.HESSIAN_GAUSS_NEWTON) is None
+
+
+def test_forced_collectives_one_rank():
+    """--rccl at N = 1: a one-rank process group (gloo in the stand-in, RCCL on a GPU) and the last step's table
+    through all_gather_into_tensor, as the N > 1 path; the line names the process group."""
+    out = _run("--standin", "--rccl", "--batch", "8", "--steps", "3", "--warmup", "1", "--no-cpu-baseline")
+    assert out["n_gpus"] == 1 and out["gathered_results_match"] is True and out["converged"] == 8
+    assert out["process_group"]["backend"] == "gloo" and out["process_group"]["world_size"] == 1
+    assert out["standin_u0_first_col"] == [float(i) for i in range(8)]
+
+
+def test_strong_rejects_batch_below_rank_count():
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--standin", "--strong", "--gpus", "3",
+                        "--batch", "2", "--steps", "1", "--warmup", "1", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert p.returncode != 0

@@ -1,0 +1,130 @@
+"""GPU: the RCCL leg of the multi-GPU path, run on the one-GPU pool.
+
+RCCL rejects two ranks on one GPU (profiles/r03/rccl/), but a ONE-rank "nccl" process group is legal, and with
+``mmpc.dist.force_collectives`` the helpers issue their collectives even at world size 1.  So every RCCL call the
+8-GPU run makes executes here on real RCCL over HIP device memory:
+  * all_gather_into_tensor of the per-instance result table (bench.py's rank-0 gather),
+  * broadcast of the shared weights / bounds (broadcast_shared),
+  * scatter of the instances and gather of the results around a real device solve (solve_rank0_batch, the
+    batched counterpart of the per-tick call ModelControl.cpp:159),
+  * all_reduce MAX / SUM (bench.py's timing and convergence reductions),
+and ``bench.py --rccl`` takes the N > 1 code path (table gathered through RCCL) at N = 1.
+The test ids carry the RCCL version the process group ran on."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, WEIGHTS_CFG
+
+pytestmark = pytest.mark.gpu
+
+
+def _rccl_version():
+    try:
+        import torch
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:
+        return "unknown"
+
+
+RCCL = _rccl_version()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture
+def rccl_group():
+    import torch
+    import torch.distributed as dist
+    from mmpc import dist as mdist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1)
+    prev = mdist.force_collectives(True)
+    try:
+        yield dist
+    finally:
+        mdist.force_collectives(prev)
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("rccl", [RCCL])
+def test_rccl_collectives_one_rank(rccl, rccl_group):
+    import torch
+    from mmpc import dist as mdist
+    dist = rccl_group
+    info = mdist.rccl_info()
+    assert info["backend"] == "nccl" and info["world_size"] == 1 and info["rccl_version"] == rccl
+    dev = torch.device("cuda", 0)
+    # the result-table gather of bench.py (uint8 rows of u_0* | status | iters)
+    res = torch.arange(4096 * 24, dtype=torch.int64, device=dev).to(torch.uint8)
+    table = torch.empty_like(res)
+    dist.all_gather_into_tensor(table, res, async_op=True).wait()
+    assert torch.equal(table, res)
+    # broadcast of the shared weights and bounds
+    w = torch.tensor(WEIGHTS_CFG, dtype=torch.float64, device=dev)
+    lb = torch.tensor([-2.0, -3.0], dtype=torch.float64, device=dev)
+    mdist.broadcast_shared(w, lb, None)
+    assert w.tolist() == WEIGHTS_CFG and lb.tolist() == [-2.0, -3.0]
+    # ragged rows through all_gather_into_tensor; scatter back
+    rows = torch.arange(37 * 3, dtype=torch.float64, device=dev).view(37, 3)
+    assert torch.equal(mdist.gather_rows(rows, 37), rows)
+    assert torch.equal(mdist.scatter_rows(rows, 37, (3,), torch.float64, dev), rows)
+    assert mdist.max_over_ranks(3.5, device=dev) == 3.5
+    assert mdist.sum_over_ranks(7, device=dev) == 7
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("rccl", [RCCL])
+def test_rccl_rank0_scatter_solve_gather(rccl, rccl_group, model_json, mmpc_mod, oracle):
+    """solve_rank0_batch on real RCCL and the HIP solver equals a direct device solve of the batch bit for bit
+    (37 instances, per-instance weights, control bounds and a warm start)."""
+    import torch
+    from mmpc import dist as mdist
+    dev = torch.device("cuda", 0)
+    N, B = 30, 37
+    x0, up, tr = oracle.synth(20250213, 0, B, N, 0.002)
+    solver = mmpc_mod.Solver(model_json(N=N))
+    NV = solver.NV
+    f64 = dict(dtype=torch.float64, device=dev)
+    w = np.tile(WEIGHTS_CFG, (B, 1)) * np.linspace(0.5, 2.0, B)[:, None]
+    args = dict(x0=torch.tensor(x0, **f64), u_prev=torch.tensor(up, **f64), traj=torch.tensor(tr, **f64),
+                weights=torch.tensor(w, **f64), weights_stride=8, V=torch.full((B, NV), 0.1, **f64),
+                u_lb=torch.tensor([-20.0, -20.0], **f64), u_ub=torch.tensor([20.0, 20.0], **f64))
+    r = mdist.solve_rank0_batch(solver, device=dev, **{k: (v.clone() if torch.is_tensor(v) else v)
+                                                        for k, v in args.items()})
+    V = args["V"].clone()
+    st = torch.empty(B, dtype=torch.int32, device=dev)
+    it = torch.empty(B, dtype=torch.int32, device=dev)
+    kk = torch.empty(B, **f64)
+    solver.solve_batch(B, args["x0"], args["u_prev"], args["traj"], args["weights"], V, st, it, kk,
+                       weights_stride=8, u_lb=args["u_lb"], u_ub=args["u_ub"])
+    torch.cuda.synchronize()
+    assert torch.equal(r["V"], V) and torch.equal(r["status"], st) and torch.equal(r["iters"], it)
+    assert torch.equal(r["kkt"], kk) and bool((st == 0).all())
+    solver.close()
+
+
+@pytest.mark.parametrize("rccl", [RCCL])
+def test_bench_rccl_flag(rccl):
+    """bench.py --rccl: the default cfg#2 step at N = 1 with the last step's table gathered through RCCL."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--rccl", "--steps", "3", "--warmup", "2",
+                        "--no-cpu-baseline", "--no-secondary", "--no-sweep"],
+                       capture_output=True, text=True, timeout=110, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    out = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["process_group"] == {"backend": "nccl", "world_size": 1, "rccl_version": rccl}
+    assert out["gathered_results_match"] is True and out["converged"] == 4096
+    assert out["zero_copy_results_checked"] is True
