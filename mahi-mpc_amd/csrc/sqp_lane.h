@@ -153,6 +153,18 @@ MMPC_HD void at_mul(T h, const T* hFq, const T* hFqd, const T* v, T* out) {
 // next stage's prefetches and all LDS traffic at each workspace access.
 template <class T>
 using gmem = __attribute__((address_space(1))) T;
+
+// A/B knobs of the stored-Jacobian change (round 4): which sweeps read the stored stage Jacobian instead of
+// evaluating the model, and where the backward sweep issues its one-stage-ahead loads
+#ifndef MMPC_LANE_JAC_BWD
+#define MMPC_LANE_JAC_BWD 1
+#endif
+#ifndef MMPC_LANE_JAC_STEP
+#define MMPC_LANE_JAC_STEP 1
+#endif
+#ifndef MMPC_LANE_PF_EARLY
+#define MMPC_LANE_PF_EARLY 0
+#endif
 __device__ __forceinline__ gmem<double>* stage_ptr(double* wsb, int64_t k, int SS, int lane) {
     gmem<double>* q = (gmem<double>*)(wsb + k * SS * 64 + lane);
     asm volatile("" : "+v"(q));
@@ -476,8 +488,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         upf[c] = s1[(FU + c) * 64];
                         umpf[c] = k1 >= 1 ? s1[(-SS + FU + c) * 64] : up[c];
                     }
+                    if (MMPC_LANE_JAC_BWD) {
 #pragma unroll
-                    for (int i = 0; i < JP; ++i) jpf[i] = s1[(SF::JAC + i) * 64];
+                        for (int i = 0; i < JP; ++i) jpf[i] = s1[(SF::JAC + i) * 64];
+                    }
                 };
 #pragma unroll
                 for (int c = 0; c < NU; ++c) unext[c] = 0.0;
@@ -500,7 +514,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                     }
 #pragma unroll
                     for (int r = 0; r < NX; ++r) rkm[r] = rpf[r];
-                    JPK::unpack(jpf, hFq, hFqd, hFu);
+                    if (MMPC_LANE_JAC_BWD) {
+                        JPK::unpack(jpf, hFq, hFqd, hFu);
+                    } else {
+                        double xd[NX];
+                        STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                    }
+                    if (MMPC_LANE_PF_EARLY && k >= 1) prefetch(k - 1);
                     // reduced gradient g_k = B_k^T lam_{k+1} + R/Rm terms (same expression as sqp_wave.h)
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
@@ -721,7 +741,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         }
                     }
                     if (k == 0) break;  // s_0 = 0: P~_0 is never used
-                    prefetch(k - 1);
+                    if (!MMPC_LANE_PF_EARLY) prefetch(k - 1);
                     // P~_k = blkdiag(A^T W + Q, R) - Y^T Y (old P is dead: overwrite it in place), p~_k = pn - Y^T yh
                     if constexpr (WLDS) {
                         // W in LDS: the a-rows of W (used by every output row) go to the dead P_xu / P_uu slots; the
@@ -895,8 +915,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         rk[r] = SK(0, SF::R, r);
                         ck[r] = SK(0, SF::C, r);
                     }
+                    if (MMPC_LANE_JAC_STEP) {
 #pragma unroll
-                    for (int i = 0; i < JP; ++i) jk[i] = SK(0, SF::JAC, i);   // A_k, B_k at this iterate (stored)
+                        for (int i = 0; i < JP; ++i) jk[i] = SK(0, SF::JAC, i);   // A_k, B_k at this iterate (stored)
+                    }
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
                         u[c] = upf[c];
@@ -953,7 +975,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                             }
                         }
                     }
-                    JPK::unpack(jk, hFq, hFqd, hFu);
+                    double Fk[NX];
+                    if (MMPC_LANE_JAC_STEP) {
+                        JPK::unpack(jk, hFq, hFqd, hFu);
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) Fk[r] = ck[r] + xpf[r];   // F_k = c_k + x_{k+1}
+                    } else {
+                        double xd[NX];
+                        STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) Fk[r] = fma(h, xd[r], x[r]);
+                    }
                     double ad[NX];
                     a_mul<NQ, NA>(h, hFq, hFqd, dx, ad);
 #pragma unroll
@@ -962,7 +994,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
-                        const double F = ck[r] + xpf[r];   // F_k = c_k + x_{k+1} (no model evaluation at the iterate)
+                        const double F = Fk[r];
                         const double qe = 2.0 * Q[r] * (F - rk[r]);
                         dJ = fma(qe, ad[r], dJ);
                         dx[r] = ad[r] + ck[r];

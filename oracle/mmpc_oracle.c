@@ -272,6 +272,50 @@ void oracle_exo_jac(const double* x, const double* u, double* A, double* B, doub
     }
 }
 
+/* The exo's Lagrangian Hessian block W = sum_r lam_r d^2 f_r / d(x,u)^2 ((nx+nu)^2 = 12 x 12, row-major; round 4,
+ * the exact-Hessian SQP on the exo).  Only the accelerations are nonlinear: with acc = M^-1 w, w = tau - D qd - G(q),
+ * mu = M^-1 lam_acc and a_j = d acc / dz_j (columns of [Fq | Fqd | Fu]), differentiating M acc = w twice gives
+ *   W_ij = sum_k mu_k d^2 w_k / dz_i dz_j - mu^T (d^2 M / dz_i dz_j) acc - mu^T (dM/dz_i) a_j - mu^T (dM/dz_j) a_i,
+ * with d^2 w_k / dq_k^2 = g_k sin q_k and the symbolic dM, d^2 M of exo_model_gen.h (nonzero for q1..q3 only). */
+void oracle_exo_hess(const double* x, const double* u, const double* lam, double* W) {
+    double M[16], dM[4][16], d2M[4][4][16], Minv[16], A[64], B[32], xd[8];
+    exo_mass_derivs(x, M, dM, d2M);
+    inv4(M, Minv);
+    oracle_exo_jac(x, u, A, B, xd);
+    const double* acc = xd + 4;
+    double mu[4], a[12][4];
+    for (int r = 0; r < 4; ++r) {
+        mu[r] = 0.0;
+        for (int c = 0; c < 4; ++c) mu[r] += Minv[r * 4 + c] * lam[4 + c];
+    }
+    for (int j = 0; j < 12; ++j)
+        for (int r = 0; r < 4; ++r) a[j][r] = j < 8 ? A[(4 + r) * 8 + j] : B[(4 + r) * 4 + (j - 8)];
+    /* nu_i = (dM/dq_i) mu (dM symmetric: mu^T dM_i v = nu_i^T v) */
+    double nu[4][4];
+    for (int i = 0; i < 4; ++i)
+        for (int r = 0; r < 4; ++r) {
+            nu[i][r] = 0.0;
+            for (int c = 0; c < 4; ++c) nu[i][r] += dM[i][r * 4 + c] * mu[c];
+        }
+    for (int i = 0; i < 12; ++i)
+        for (int j = 0; j < 12; ++j) {
+            double t = 0.0;
+            if (i < 4 && j < 4) {
+                if (i == j) t += mu[i] * EXO_GRAVITY_GAIN[i] * sin(x[i]);
+                for (int r = 0; r < 4; ++r) {
+                    double m = 0.0;
+                    for (int c = 0; c < 4; ++c) m += d2M[i][j][r * 4 + c] * acc[c];
+                    t -= mu[r] * m;
+                }
+            }
+            if (i < 4)
+                for (int r = 0; r < 4; ++r) t -= nu[i][r] * a[j][r];
+            if (j < 4)
+                for (int r = 0; r < 4; ++r) t -= nu[j][r] * a[i][r];
+            W[i * 12 + j] = t;
+        }
+}
+
 void oracle_exo_mass(const double* q, double* M) {
     double dM[4][16];
     exo_mass_and_grad(q, M, dM);
@@ -292,12 +336,13 @@ int oracle_set_user_model_hess(oracle_user_hess_fn hess) {
     return 0;
 }
 static int model_has_hess(void) {
-    if (t_model == ORACLE_MODEL_TWO_LINK_ARM) return 1;
+    if (t_model == ORACLE_MODEL_TWO_LINK_ARM || t_model == ORACLE_MODEL_EXO_ARM) return 1;
     if (t_model == ORACLE_MODEL_USER) return g_user_hess != NULL;
     return 0;
 }
 static int model_hess(const double* x, const double* u, const double* lam, double* W) {
     if (t_model == ORACLE_MODEL_TWO_LINK_ARM) { oracle_two_link_hess(x, u, lam, W); return 1; }
+    if (t_model == ORACLE_MODEL_EXO_ARM) { oracle_exo_hess(x, u, lam, W); return 1; }
     if (t_model == ORACLE_MODEL_USER && g_user_hess) { g_user_hess(x, u, lam, W); return 1; }
     return 0;
 }

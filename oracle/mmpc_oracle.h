@@ -75,6 +75,8 @@ void oracle_two_link_jac(const double* x, const double* u, double* A, double* B,
  * A = df/dx (8x8), B = df/du (8x4) row-major, xdot; and the mass matrix M(q) (4x4 row-major) */
 void oracle_exo_jac(const double* x, const double* u, double* A, double* B, double* xdot);
 void oracle_exo_mass(const double* q, double* M);
+/* W = sum_r lam_r d^2 f_r / d(x,u)^2 of the exo (12 x 12 row-major; lam: [nx]) */
+void oracle_exo_hess(const double* x, const double* u, const double* lam, double* W);
 /* linearised Euler step F_lin, ModelGenerator.cpp:47-48 (A,B row-major here) */
 void oracle_f_lin(int nx, int nu, double h, const double* A, const double* B, const double* x,
                   const double* u, const double* xdot_init, const double* x_init,

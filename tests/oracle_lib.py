@@ -58,6 +58,7 @@ def lib():
         L.oracle_synth_exo.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int, C.c_double, _dp, _dp, _dp]
         L.oracle_exo_jac.argtypes = [_dp, _dp, _dp, _dp, _dp]
         L.oracle_exo_mass.argtypes = [_dp, _dp]
+        L.oracle_exo_hess.argtypes = [_dp, _dp, _dp, _dp]
         L.oracle_two_link_hess.argtypes = [_dp, _dp, _dp, _dp]
         L.oracle_set_hessian.argtypes = [C.c_int]
         L.oracle_set_kkt.argtypes = [C.c_int]

@@ -95,3 +95,45 @@ def test_linear_mode_single_iteration(oracle):
     w = np.array([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4)
     r = oracle.solve_batch(N, h, x0, up, tr, w, model=oracle.EXO, is_linear=True)
     assert (r["status"] == 0).all() and (r["iters"] <= 2).all()
+
+
+def test_exo_lagrangian_hessian_matches_jacobian_differences(oracle):
+    """oracle_exo_hess (analytic: d^2 acc from M acc = w differentiated twice, symbolic dM and d^2M of
+    exo_model_gen.h) equals central differences of lam^T [A | B] of the oracle's analytic exo Jacobian, and is
+    symmetric (round 4: the exact-Hessian SQP on the exo, IPOPT's default nlp_hess_l, ModelGenerator.cpp:238)."""
+    L = oracle.lib()
+    rng = np.random.default_rng(1)
+    for _ in range(10):
+        x, u, lam = rng.uniform(-1, 1, 8), rng.uniform(-2, 2, 4), rng.uniform(-3, 3, 8)
+        W = np.zeros(144)
+        L.oracle_exo_hess(x, u, lam, W)
+        W = W.reshape(12, 12)
+
+        def g(z):
+            A, B, xd = np.zeros(64), np.zeros(32), np.zeros(8)
+            L.oracle_exo_jac(z[:8].copy(), z[8:].copy(), A, B, xd)
+            return lam @ np.hstack([A.reshape(8, 8), B.reshape(8, 4)])
+        z, h = np.concatenate([x, u]), 1e-6
+        Wf = np.stack([(g(z + h * e) - g(z - h * e)) / (2 * h) for e in np.eye(12)], axis=1)
+        assert np.abs(W - Wf).max() <= 1e-7 * max(1.0, np.abs(Wf).max())
+        assert np.abs(W - W.T).max() <= 1e-14 * max(1.0, np.abs(W).max())
+        # only the q rows/columns are nonzero past the q-q block: d^2 acc / dqd^2 = d^2 acc / dtau^2 = 0
+        assert np.abs(W[4:, 4:]).max() == 0.0
+
+
+def test_exo_exact_hessian_same_kkt_point(oracle):
+    """Exact-Hessian SQP on the exo reaches the Gauss-Newton KKT point (the build's exo AUTO stays Gauss-Newton:
+    on cfg#3 instances the exact Hessian takes more iterations)."""
+    N, h = 50, 0.002
+    x0, up, tr = oracle.synth(20250213, 0, 64, N, h, model=oracle.EXO)
+    w = np.array([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4)
+    gn = oracle.solve_batch(N, h, x0, up, tr, w, model=oracle.EXO, init_states=2, kkt=oracle.KKT_RICCATI)
+    ex = oracle.solve_batch(N, h, x0, up, tr, w, model=oracle.EXO, init_states=2, kkt=oracle.KKT_RICCATI,
+                            hessian=oracle.HESS_EXACT)
+    dense = oracle.solve_batch(N, h, x0, up, tr, w, model=oracle.EXO, init_states=2, hessian=oracle.HESS_EXACT)
+    assert (gn["status"] == 0).all() and (ex["status"] == 0).all() and (dense["status"] == 0).all()
+    scale = np.abs(gn["V"]).max(axis=1)
+    assert (np.abs(ex["V"] - gn["V"]).max(axis=1) / scale).max() <= 1e-7
+    # the Riccati restatement of the exact QP reproduces the dense one
+    assert (ex["iters"] == dense["iters"]).all()
+    assert (np.abs(ex["V"] - dense["V"]).max(axis=1) / scale).max() <= 1e-10

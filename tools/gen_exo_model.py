@@ -188,6 +188,20 @@ def main():
             ndmono += n
             dlines.append(f"        dM[{i}] = {e};")
         dlines.append("    }")
+    # second derivatives d^2 M / dq_I dq_J (1 <= I <= J <= 3) for the exact Lagrangian Hessian of the exo
+    # (round 4: mmpc_opts.hessian = EXACT on the exo model)
+    pairs = [(a, b) for a in range(3) for b in range(a, 3)]
+    d2polys = {}
+    for a, b in pairs:
+        d2polys[(a, b)] = [sp.expand(-s[a] * sp.diff(pe, c[a]) + c[a] * sp.diff(pe, s[a])) for pe in dpolys[b]]
+    d2lines, nd2mono = [], 0
+    for a, b in pairs:
+        d2lines.append(f"    if (I == {a + 1} && J == {b + 1}) {{")
+        for i, pe in enumerate(d2polys[(a, b)]):
+            e, n = emit_poly(pe)
+            nd2mono += n
+            d2lines.append(f"        d2M[{i}] = {e};")
+        d2lines.append("    }")
     pw = []
     for v, e in sorted(used):
         pw.append(f"        {v}_{e} = " + " * ".join([v] * e) + ";")
@@ -246,6 +260,16 @@ __device__ __forceinline__ void dmass_upper(const TrigPowers& t, double* dM) {{
 {chr(10).join(dlines)}
 }}
 
+// d^2 M / dq_I dq_J (1 <= I <= J <= 3), upper triangle ({nd2mono} monomials; the exact exo Hessian)
+template <int I, int J>
+__device__ __forceinline__ void d2mass_upper(const TrigPowers& t, double* d2M) {{
+    static_assert(1 <= I && I <= J && J <= 3, "I <= J in 1..3");
+    cdouble* const K = coef_table();
+    [[maybe_unused]] const double c1 = t.c1, c2 = t.c2, c3 = t.c3, s1 = t.s1, s2 = t.s2, s3 = t.s3;
+    [[maybe_unused]] const double {unpack};
+{chr(10).join(d2lines)}
+}}
+
 }}  // namespace exo
 }}  // namespace mmpc
 """
@@ -261,6 +285,8 @@ __device__ __forceinline__ void dmass_upper(const TrigPowers& t, double* dM) {{
         for pexpr in polys:
             d = -s[j] * sp.diff(pexpr, c[j]) + c[j] * sp.diff(pexpr, s[j])
             exprs.append(sp.expand(d))
+    for a, b in pairs:
+        exprs.extend(d2polys[(a, b)])
     repl2, red2 = sp.cse(exprs, symbols=sp.numbered_symbols("t"), optimizations="basic")
     ol = []
     for sym, ex in repl2:
@@ -280,18 +306,31 @@ __device__ __forceinline__ void dmass_upper(const TrigPowers& t, double* dM) {{
 static const double EXO_GRAVITY_GAIN[4] = {{{", ".join(lit(sp.Rational(v)) for v in pj["gravity_gain"])}}};
 static const double EXO_DAMPING[4] = {{{", ".join(lit(sp.Rational(v)) for v in pj["damping"])}}};
 
-/* M[16] row-major, dM[j][16] = dM/dq_j (dM[0] = 0: M does not depend on q0) */
-static void exo_mass_and_grad(const double* q, double* M, double dM[4][16]) {{
+/* M[16] row-major, dM[j][16] = dM/dq_j (dM[0] = 0: M does not depend on q0); d2M (may be NULL) [4][4][16] =
+ * d^2 M / dq_i dq_j (zero where i or j is 0) */
+static void exo_mass_derivs(const double* q, double* M, double dM[4][16], double d2M[4][4][16]) {{
     const double c1 = cos(q[1]), s1 = sin(q[1]), c2 = cos(q[2]), s2 = sin(q[2]), c3 = cos(q[3]), s3 = sin(q[3]);
-    double up[40];
+    double up[{10 + 30 + 60}];
 {chr(10).join(ol)}
     static const int ia[10] = {{0, 0, 0, 0, 1, 1, 1, 2, 2, 3}}, ib[10] = {{0, 1, 2, 3, 1, 2, 3, 2, 3, 3}};
+    static const int pa[6] = {{1, 1, 1, 2, 2, 3}}, pb[6] = {{1, 2, 3, 2, 3, 3}};
     for (int j = 0; j < 16; ++j) dM[0][j] = 0.0;
+    if (d2M)
+        for (int a = 0; a < 4; ++a)
+            for (int b = 0; b < 4; ++b)
+                for (int j = 0; j < 16; ++j) d2M[a][b][j] = 0.0;
     for (int t = 0; t < 10; ++t) {{
         M[ia[t] * 4 + ib[t]] = M[ib[t] * 4 + ia[t]] = up[t];
         for (int j = 0; j < 3; ++j) dM[j + 1][ia[t] * 4 + ib[t]] = dM[j + 1][ib[t] * 4 + ia[t]] = up[10 + 10 * j + t];
+        if (d2M)
+            for (int p = 0; p < 6; ++p) {{
+                const double v = up[40 + 10 * p + t];
+                d2M[pa[p]][pb[p]][ia[t] * 4 + ib[t]] = d2M[pa[p]][pb[p]][ib[t] * 4 + ia[t]] = v;
+                d2M[pb[p]][pa[p]][ia[t] * 4 + ib[t]] = d2M[pb[p]][pa[p]][ib[t] * 4 + ia[t]] = v;
+            }}
     }}
 }}
+static void exo_mass_and_grad(const double* q, double* M, double dM[4][16]) {{ exo_mass_derivs(q, M, dM, NULL); }}
 #endif
 """
     open(os.path.join(REPO, "oracle", "exo_model_gen.h"), "w").write(orc)
@@ -330,7 +369,7 @@ static void exo_mass_and_grad(const double* q, double* M, double dM[4][16]) {{
                "method": "sympy parse of the printed expressions, evaluated with 40-digit mpmath, no expansion",
                "min_eigenvalue_over_2000_random_q": worst, "monomials": nterms, "cases": kat},
               open(os.path.join(REPO, "tests", "golden", "exo_mass_kat.json"), "w"), indent=1)
-    print(f"monomials {nterms} (M) / {ndmono} (dM), oracle cse temps {len(repl2)}, min eig {worst:.3e}")
+    print(f"monomials {nterms} (M) / {ndmono} (dM) / {nd2mono} (d2M), oracle cse temps {len(repl2)}, min eig {worst:.3e}")
 
 
 if __name__ == "__main__":

@@ -37,5 +37,10 @@ for (h, d), seg in loops.items():
     gl = sum(v for k, v in c.items() if k.startswith("global_"))
     dpp = sum(v for k, v in c.items() if "dpp" in k)
     cnd = sum(v for k, v in c.items() if "cndmask" in k)
+    scr = sum(v for k, v in c.items() if k.startswith("scratch_"))
+    acc = sum(v for k, v in c.items() if k.startswith("v_accvgpr"))
+    lane = sum(v for k, v in c.items() if k.startswith(("v_readlane", "v_writelane")))
+    vmw = sum(1 for x in seg if x.startswith("s_waitcnt") and "vmcnt" in x)
     print(f"{h:8s} depth {d} instr {len(seg):4d}  f64 {f64:3d}  dpp {dpp:3d}  cndmask {cnd:3d}  ds {ds:3d}  "
-          f"global {gl:3d}  salu {salu:3d}  other {len(seg) - f64 - dpp - cnd - ds - gl - salu:3d}")
+          f"global {gl:3d}  scratch {scr:3d}  accvgpr {acc:3d}  r/wlane {lane:3d}  vmcnt-waits {vmw:3d}  salu {salu:3d}  "
+          f"other {len(seg) - f64 - dpp - cnd - ds - gl - salu - scr - acc - lane:3d}")

@@ -3,9 +3,15 @@
 // per wave) and the wall time give cycles per wave-instruction for one wave alone and for co-resident waves:
 //   f64 fma | f64 mul | f32 fma | v_mov_b64_dpp row_newbcast | dpp + f64 fma pair | u32 add
 // Decides whether a second wave per SIMD adds FP64 issue bandwidth (SIMD-32: a wave64 instruction is 2 passes).
+// Round 4: R = 32768 steps (262,144 instructions per wave, ~1 ms) so the ~6 us launch overhead no longer inflates the
+// wall-clock "SIMD throughput" column (round 3 ran R = 512: 4,096 instructions, 13-44 us kernels); the effective
+// shader clock (s_memtime cycles / wall time) is printed so both columns are in the same cycles.
 #include <hip/hip_runtime.h>
 #include <cstdio>
-constexpr int R = 512;
+#ifndef R_STEPS
+#define R_STEPS 32768
+#endif
+constexpr int R = R_STEPS;
 template <int L> __device__ __forceinline__ double bc(double v) { return __builtin_amdgcn_update_dpp(v, v, 0x150 + L, 0xf, 0xf, true); }
 
 template <int OP>
@@ -56,9 +62,11 @@ void run(const char* name, double* d, long long* c) {
     for (int i = 0; i < grid; ++i) mean += h[i];
     mean /= grid;
     const double per_wave = mean / (R * 8.0);                       // wave's own cycles per instruction
-    const double wall_simd = ms * 1e-3 * 2.4e9 * 1024 / (grid * R * 8.0);  // SIMD cycles per wave-instr @2.4 GHz
-    printf("%-28s waves/SIMD %d: per-wave %6.2f cyc/instr, SIMD throughput %6.2f cyc/instr (wall %.3f ms)\n", name,
-           grid / 1024, per_wave, wall_simd, ms);
+    const double clk = mean / (ms * 1e-3);                          // s_memtime cycles per second of wall time
+    const double wall_simd = ms * 1e-3 * clk * 1024 / (grid * R * 8.0);  // SIMD cycles per wave-instr, same clock
+    printf("%-28s waves/SIMD %d: per-wave %6.2f cyc/instr, per-wave / waves %6.2f, SIMD throughput (wall) %6.2f "
+           "cyc/instr, clock %.2f GHz (wall %.3f ms)\n", name, grid / 1024, per_wave, per_wave / (grid / 1024), wall_simd,
+           clk * 1e-9, ms);
     hipEventDestroy(e0);
     hipEventDestroy(e1);
   }
