@@ -527,6 +527,8 @@ def run_config(args, name, world, rank, primary=True):
                                  and args.hessian == "auto"))):
         # the exo solve at the reference's IPOPT tolerance (ModelControl.cpp:54) beside the line's 1e-8 / 1e-10
         out["tolerance_sweep"] = cfg5_sweep(path, cfg, n, x0, up, tr, w, "auto", fp32=False)
+        # and with IPOPT's exact Hessian (the line runs Gauss-Newton, the exo's AUTO choice): iteration histograms
+        out["exact_hessian"] = hessian_compare(path, n, x0, up, tr, w, V, iters)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not standin and name != "cfg5":
         out["cpu_baseline"] = cpu_baseline(cfg, N, h, args.cpu_seconds, V.cpu().numpy(), iters, tol_grad,
                                            tol_defect, hess, None if ulb is None else args.u_bound,
@@ -582,6 +584,39 @@ def cfg5_sweep(path, cfg, B, x0, up, tr, w, hessian, reps=5, fp32=True):
                  "mean_iters": float(it_ref.mean()), "max_iters": int(it_ref.max()), "kernel_ms": t_ref,
                  "solves_per_s_kernel": B / (t_ref * 1e-3), "max_rel_V_vs_fp64": 0.0})
     return rows
+
+
+def hessian_compare(path, B, x0, up, tr, w, V_gn, it_gn, reps=3):
+    """The same batch with the exact Lagrangian Hessian (mmpc_opts.hessian = EXACT; IPOPT's default, nlp_hess_l at
+    ModelGenerator.cpp:238) beside the line's Hessian: iteration histograms, kernel ms (HIP events, median of `reps`
+    after one untimed solve) and the largest relative difference of the solutions (same KKT point)."""
+    import torch
+    import mmpc
+    s = mmpc.Solver(path, hessian=mmpc.HESSIAN_EXACT, init_states=mmpc.INIT_ZERO)
+    s.reserve_workspace(B)
+    V = torch.zeros((B, s.NV), dtype=torch.float64, device=x0.device)
+    st = torch.zeros(B, dtype=torch.int32, device=x0.device)
+    it = torch.zeros(B, dtype=torch.int32, device=x0.device)
+    times = []
+    for r in range(reps + 1):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        s.solve_batch(B, x0, up, tr, w, V, st, it, None)
+        e1.record()
+        torch.cuda.synchronize()
+        if r:
+            times.append(e0.elapsed_time(e1))
+    ksolver = s.kkt_solver_for(B)
+    s.close()
+    hist = lambda a: {int(k): int(v) for k, v in zip(*np.unique(a, return_counts=True))}  # noqa: E731
+    itn, stn = it.cpu().numpy(), st.cpu().numpy()
+    scale = torch.clamp(V_gn.abs().amax(dim=1), min=1e-300)
+    return {"hessian": "exact (Lagrangian, IPOPT's default)",
+            "kkt_solver": {2: "riccati (lane per instance)", 3: "riccati (16 lanes per instance)"}.get(ksolver, ksolver),
+            "converged": int((stn == 0).sum()), "mean_iters": float(itn.mean()), "max_iters": int(itn.max()),
+            "iters_hist": hist(itn), "kernel_ms": float(np.median(times)),
+            "line_hessian_iters_hist": hist(it_gn),
+            "max_rel_V_vs_line": float(((V - V_gn).abs().amax(dim=1) / scale).max().item())}
 
 
 def model_flops_per_iteration(mmpc, cfg, ksolver, N, hess):

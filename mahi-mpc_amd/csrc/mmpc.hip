@@ -626,25 +626,30 @@ struct ExactDefault<M, std::enable_if_t<!M::kExactDefault || M::kExactDefault>> 
 int resolve_hessian(const mmpc_handle* h, int solver, bool u_bounded) {
     const int want = h->opts.hessian;
     if (want == MMPC_HESSIAN_GAUSS_NEWTON) return MMPC_HESSIAN_GAUSS_NEWTON;
-    bool capable = false, dflt = false;
+    bool group_capable = false, lane_capable = false, dflt = false;
     with_model(h->info.model_id, [&](auto* m) {
         using M = std::remove_pointer_t<decltype(m)>;
-        capable = exact_capable<M>();
+        group_capable = exact_capable<M>();
+        lane_capable = HasHess<M>::value;
         dflt = ExactDefault<M>::value;
         return MMPC_OK;
     });
-    // control bounds (the projected SQP): EXACT fixes the held controls in the exact QP as in the Gauss-Newton one;
-    // AUTO keeps Gauss-Newton there -- measured faster at cfg#2 with +-2 Nm (0.77 vs 0.91 ms: the exact solves take
-    // fewer iterations, but every re-solve after a hold repeats the costlier exact Riccati sweep)
-    const bool ok = capable && solver == MMPC_KKT_RICCATI_GROUP && !h->x_bounded && !h->info.is_linear &&
-                    !h->opts.factor_fp32;
+    // control bounds (the projected SQP): EXACT fixes the held controls in the exact QP as in the Gauss-Newton one
+    // (group kernel); AUTO keeps Gauss-Newton there -- measured faster at cfg#2 with +-2 Nm (0.77 vs 0.91 ms: the
+    // exact solves take fewer iterations, but every re-solve after a hold repeats the costlier exact Riccati sweep,
+    // DESIGN.md 3b).  The lane kernel (round 4) takes EXACT for unbounded solves on request; AUTO there stays
+    // Gauss-Newton (its backward sweep evaluates the model's Hessian per stage).
+    const bool common = !h->x_bounded && !h->info.is_linear && !h->opts.factor_fp32;
+    const bool group_ok = common && group_capable && solver == MMPC_KKT_RICCATI_GROUP;
+    const bool lane_ok = common && lane_capable && solver == MMPC_KKT_RICCATI && !u_bounded;
     if (want == MMPC_HESSIAN_EXACT) {
-        if (!ok)
-            return fail(MMPC_ERR_UNSUPPORTED, "exact Hessian: needs a model with second derivatives, the "
-                                              "RICCATI_GROUP solver and a nonlinear solve without state bounds");
+        if (!group_ok && !lane_ok)
+            return fail(MMPC_ERR_UNSUPPORTED, "exact Hessian: needs a model with second derivatives, a Riccati "
+                                              "solver (RICCATI_GROUP; RICCATI without control bounds) and a "
+                                              "nonlinear solve without state bounds");
         return MMPC_HESSIAN_EXACT;
     }
-    return ok && dflt && !u_bounded ? MMPC_HESSIAN_EXACT : MMPC_HESSIAN_GAUSS_NEWTON;
+    return group_ok && dflt && !u_bounded ? MMPC_HESSIAN_EXACT : MMPC_HESSIAN_GAUSS_NEWTON;
 }
 
 template <class Model, bool BOUNDED, bool XB = false, bool EXACT = false>
@@ -656,7 +661,14 @@ int launch_group(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const So
 }
 
 template <class Model, class FT>
-void launch_lane(bool bounded, bool xb, dim3 grid, dim3 block, hipStream_t stream, const SolveParams& p, LaneWork lw) {
+void launch_lane(bool bounded, bool xb, dim3 grid, dim3 block, hipStream_t stream, const SolveParams& p, LaneWork lw,
+                 bool exact = false) {
+    if constexpr (HasHess<Model>::value && std::is_same<FT, double>::value) {
+        if (exact && !bounded && !xb) {
+            sqp_lane_kernel<Model, double, false, false, true><<<grid, block, 0, stream>>>(p, lw);
+            return;
+        }
+    }
     if (xb) sqp_lane_kernel<Model, FT, false, true><<<grid, block, 0, stream>>>(p, lw);
     else if (bounded) sqp_lane_kernel<Model, FT, true><<<grid, block, 0, stream>>>(p, lw);
     else sqp_lane_kernel<Model, FT, false><<<grid, block, 0, stream>>>(p, lw);
@@ -770,10 +782,8 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
     }
     if (p.x_bounded && solver == MMPC_KKT_CONDENSED)
         return fail(MMPC_ERR_UNSUPPORTED, "state bounds need a Riccati solver (MMPC_KKT_RICCATI[_GROUP])");
-    {
-        const int hess = resolve_hessian(h, solver, bounded);   // EXACT requested on an unsupported solver
-        if (hess < 0) return hess;
-    }
+    const int hess = resolve_hessian(h, solver, bounded);   // EXACT requested on an unsupported solver: error
+    if (hess < 0) return hess;
     if (solver == MMPC_KKT_CONDENSED) {
         if (h->opts.factor_fp32) return fail(MMPC_ERR_UNSUPPORTED, "factor_fp32 is a Riccati-solver option");
 #if MMPC_BUILTIN_MODELS
@@ -802,7 +812,7 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
             if (f32) launch_lane<M, float>(bounded, p.x_bounded != 0, grid, block, stream, p, lw);
-            else launch_lane<M, double>(bounded, p.x_bounded != 0, grid, block, stream, p, lw);
+            else launch_lane<M, double>(bounded, p.x_bounded != 0, grid, block, stream, p, lw, hess == MMPC_HESSIAN_EXACT);
             return MMPC_OK;
         });
         if (rc) return rc;

@@ -192,6 +192,88 @@ struct ExoArm {
         }
     }
 
+    // W = sum_s lam[s] d^2 acc_s / d(x, u)^2 (12 x 12 row-major over z = (q, qd, tau)): the dynamics part of the
+    // Lagrangian Hessian (CasADi nlp_hess_l, ModelGenerator.cpp:238).  Differentiating M acc = w (w = tau - D qd -
+    // G(q)) twice, with mu = M^-1 lam, rho_i = M^-1 (dM/dq_i) mu and beta_j = (dM/dq_j) acc:
+    //   W_{q_i q_j}   = delta_ij mu_i g_i sin q_i - mu^T (d^2M/dq_i dq_j) acc + rho_i.beta_j + rho_j.beta_i
+    //                   + g_j cos q_j rho_i[j] + g_i cos q_i rho_j[i]
+    //   W_{q_i qd_j}  = D_j rho_i[j],   W_{q_i tau_j} = -rho_i[j],   all qd / tau blocks 0
+    // (the oracle's oracle_exo_hess states the same with a Gauss-Jordan inverse and dense loops).
+    static constexpr bool kHasHess = true;
+    static constexpr bool kControlAffine = true;    // d^2 acc / dtau^2 = 0
+    static constexpr bool kExactDefault = false;    // AUTO keeps Gauss-Newton: more iterations exact
+    MMPC_HD static void eval_hess(const double* x, const double* u, const double* lam, double* W) {
+        double s[4], c[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sincos(x[i], &s[i], &c[i]);
+        const exo::TrigPowers tp(c[1], c[2], c[3], s[1], s[2], s[3]);
+        double Mu[10], l[10], il[4], w[4], acc[4], mu[4];
+        exo::mass_upper(tp, Mu);
+        chol4(Mu, l, il);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = u[i] - exo::kDamping[i] * x[4 + i] - exo::kGravityGain[i] * s[i];
+        chol4_solve(l, il, w, acc);
+        chol4_solve(l, il, lam, mu);
+        double beta[4][4], rho[4][4];   // [0] = 0: M does not depend on q0
+#pragma unroll
+        for (int r = 0; r < 4; ++r) beta[0][r] = rho[0][r] = 0.0;
+        {
+            double nu[4];
+            dmass_times<1>(tp, acc, beta[1]);
+            dmass_times<1>(tp, mu, nu);
+            chol4_solve(l, il, nu, rho[1]);
+            dmass_times<2>(tp, acc, beta[2]);
+            dmass_times<2>(tp, mu, nu);
+            chol4_solve(l, il, nu, rho[2]);
+            dmass_times<3>(tp, acc, beta[3]);
+            dmass_times<3>(tp, mu, nu);
+            chol4_solve(l, il, nu, rho[3]);
+        }
+        // mu^T (d^2M/dq_i dq_j) acc for 1 <= i <= j <= 3
+        double h2[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) h2[i][j] = 0.0;
+        d2_bilinear<1, 1>(tp, mu, acc, h2);
+        d2_bilinear<1, 2>(tp, mu, acc, h2);
+        d2_bilinear<1, 3>(tp, mu, acc, h2);
+        d2_bilinear<2, 2>(tp, mu, acc, h2);
+        d2_bilinear<2, 3>(tp, mu, acc, h2);
+        d2_bilinear<3, 3>(tp, mu, acc, h2);
+#pragma unroll
+        for (int i = 0; i < 144; ++i) W[i] = 0.0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int j = i; j < 4; ++j) {
+                double t = -h2[i][j];
+                if (i == j) t = fma(mu[i] * exo::kGravityGain[i], s[i], t);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) t = fma(rho[i][r], beta[j][r], fma(rho[j][r], beta[i][r], t));
+                t = fma(exo::kGravityGain[j] * c[j], rho[i][j], t);
+                t = fma(exo::kGravityGain[i] * c[i], rho[j][i], t);
+                W[i * 12 + j] = W[j * 12 + i] = t;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                W[i * 12 + 4 + j] = W[(4 + j) * 12 + i] = exo::kDamping[j] * rho[i][j];
+                W[i * 12 + 8 + j] = W[(8 + j) * 12 + i] = -rho[i][j];
+            }
+        }
+    }
+    // out[I][J] = out[J][I] = a^T (d^2M/dq_I dq_J) b
+    template <int I, int J>
+    MMPC_HD static void d2_bilinear(const exo::TrigPowers& tp, const double* a, const double* b, double (*out)[4]) {
+        double d[10], v[4];
+        exo::d2mass_upper<I, J>(tp, d);
+        v[0] = fma(d[0], b[0], fma(d[1], b[1], fma(d[2], b[2], d[3] * b[3])));
+        v[1] = fma(d[1], b[0], fma(d[4], b[1], fma(d[5], b[2], d[6] * b[3])));
+        v[2] = fma(d[2], b[0], fma(d[5], b[1], fma(d[7], b[2], d[8] * b[3])));
+        v[3] = fma(d[3], b[0], fma(d[6], b[1], fma(d[8], b[2], d[9] * b[3])));
+        out[I][J] = out[J][I] = fma(a[0], v[0], fma(a[1], v[1], fma(a[2], v[2], a[3] * v[3])));
+    }
+
     MMPC_HD static void eval_jac(const double* x, const double* u, double* xd, double* fx, double* fu) {
         double qdd[4], Fq[16], Fqd[16], Fu[16];
         eval_acc_jac(x, u, qdd, Fq, Fqd, Fu);

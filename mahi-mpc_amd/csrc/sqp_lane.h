@@ -175,12 +175,18 @@ __device__ __forceinline__ gmem<double>* stage_ptr(double* wsb, int64_t k, int S
 // recursion, P in LDS, the gains K and the W scratch in fp32; model evaluations, defects, adjoint, gradient,
 // merit and iterates stay fp64, so every SQP iteration refines the fp32 step against fp64 residuals).
 // XB: state bounds, the primal-dual interior-point variant (oracle solve_one_ip; see sqp_group.h)
-template <class Model, class FT = double, bool BOUNDED = false, bool XB = false>
+// EXACT: the exact Lagrangian Hessian (IPOPT's default, CasADi nlp_hess_l at ModelGenerator.cpp:238; oracle
+// solve_one_riccati with ORACLE_HESS_EXACT): the backward step of stage k adds W_k = h sum_s lam_{k+1,NQ+s}
+// d^2 acc_s / d(x_k,u_k)^2 (Model::eval_hess at the iterate, lam the adjoint of this sweep) to H_ww, H_wx and the x
+// block of P~_k; a sweep whose H_ww is not positive definite is redone without W (the Gauss-Newton step)
+template <class Model, class FT = double, bool BOUNDED = false, bool XB = false, bool EXACT = false>
 // one wave per SIMD by design (P~ in LDS, ~40 KB per wave): telling the scheduler so lets it schedule for latency
 // rather than for a second wave's registers (cfg#3: 12.06 -> 11.94 ms)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_lane_kernel(SolveParams p,
                                                                                                  LaneWork lw) {
     static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
+    static_assert(!EXACT || (HasHess<Model>::value && std::is_same<FT, double>::value && !BOUNDED && !XB),
+                  "exact Hessian: unbounded fp64 solves of models with second derivatives");
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
     constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)
     static_assert(NQ >= 0 && NA >= NQ, "x = [q; z] with qdot = z[0:NQ]");
@@ -443,6 +449,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         #pragma unroll 1
         for (int pass = 0;; ++pass) {
             bool resolve = false;
+            bool useW = EXACT;   // exact-Hessian blocks in this sweep (false: the Gauss-Newton retry)
+            #pragma unroll 1
+            for (;;) {
             gmax = 0.0;
             lmax = 0.0;
             fact_ok = true;
@@ -521,6 +530,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
                     }
                     if (MMPC_LANE_PF_EARLY && k >= 1) prefetch(k - 1);
+                    // exact Hessian: W_k at (x_k, u_k) with lam_{k+1} (lam holds it until the adjoint step below)
+                    constexpr int KZ = NX + NU;
+                    double Wk[EXACT ? KZ * KZ : 1];
+                    if constexpr (EXACT) {
+                        if (useW) {
+                            double la[NA];
+#pragma unroll
+                            for (int s2 = 0; s2 < NA; ++s2) la[s2] = h * lam[NQ + s2];
+                            Model::eval_hess(x, u, la, Wk);
+                        } else {
+#pragma unroll
+                            for (int i = 0; i < KZ * KZ; ++i) Wk[i] = 0.0;
+                        }
+                    }
                     // reduced gradient g_k = B_k^T lam_{k+1} + R/Rm terms (same expression as sqp_wave.h)
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
@@ -600,6 +623,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                                 t = fma(fu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), fu[s * NU + b], t));
                             if (a == b) t += (FT)(R[a] + Rm[a]);
                             if (XB && a == b) t += (FT)SK(0, SF::SG, NX + a);
+                            if constexpr (EXACT) t += Wk[(NX + a) * KZ + NX + b];
                             Hww[a][b] = t;
                         }
                         double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
@@ -613,6 +637,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                         for (int r = 0; r < NX; ++r) ga[r] = G[r][a];
                         at_mul<NQ, NA, FT>(hf, fq, fqd, ga, &Y[a][0]);  // H_wx row a = (A^T G[:, a])^T
+                        if constexpr (EXACT) {   // + W_ux row a
+#pragma unroll
+                            for (int j = 0; j < NX; ++j) Y[a][j] += Wk[(NX + a) * KZ + j];
+                        }
 #pragma unroll
                         for (int c = 0; c < NU; ++c) Y[a][NX + c] = (FT)((a == c) ? -R[a] : 0.0);
                     }
@@ -760,6 +788,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         }
                         auto out = [&](int a, int b, FT v) {
                             v += (FT)((a == b) ? Q[a] + (XB ? SK(-1, SF::SG, a) : 0.0) : 0.0);
+                            if constexpr (EXACT) v += Wk[a * KZ + b];   // + W_xx
 #pragma unroll
                             for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
                             PS(a, b) = v;
@@ -806,6 +835,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                         for (int a = 0; a <= b; ++a) {
                             FT v = col[a] + (FT)((a == b) ? Q[a] + (XB ? SK(-1, SF::SG, a) : 0.0) : 0.0);
+                            if constexpr (EXACT) v += Wk[a * KZ + b];   // + W_xx
 #pragma unroll
                             for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
                             PS(a, b) = v;
@@ -828,6 +858,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         }
                     }
                 }
+            }
+            // exact KKT matrix not positive definite on the null space: this iteration takes the Gauss-Newton step
+            if (!(EXACT && useW && !fact_ok)) break;
+            useW = false;
             }
             MMPC_PHASE(2);
             if (pass == 0) {

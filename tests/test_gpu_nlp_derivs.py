@@ -107,8 +107,8 @@ def test_nlp_derivs_generated_model(mmpc_mod, oracle):
 def test_nlp_hess(model, mmpc_mod, oracle, tmp_path):
     """mmpc_nlp_hess_batch (nlp_hess_l, ModelGenerator.cpp:238): the (x_k, u_k) stage blocks of the Hessian of
     lam_f J + lam_g^T g against the oracle's (its own hyper-dual second derivatives for the 2-link arm; the host build
-    of the generated header, itself pinned to sympy, for cart-pole) at 1e-12 relative; symmetric.  The exo model has
-    no second derivatives: an API error, not a silent Gauss-Newton block."""
+    of the generated header, itself pinned to sympy, for cart-pole; round 4: the exo's analytic Hessian, oracle_exo_hess,
+    itself checked against differences of the analytic Jacobian) at 1e-12 relative; symmetric."""
     B, lam_f = 24, 0.7
     if model == "cart_pole":
         path = os.path.join(ROOT, "mahi-mpc_amd", "lib", "user", "cart_pole.json")
@@ -130,11 +130,6 @@ def test_nlp_hess(model, mmpc_mod, oracle, tmp_path):
     f = dict(dtype=torch.float64, device="cuda")
     t = lambda a: torch.tensor(np.ascontiguousarray(a), **f)  # noqa: E731
     out = torch.zeros((B, N, K, K), **f)
-    if model == "exo_arm":
-        with pytest.raises(mmpc_mod.MmpcError) as ei:
-            s.nlp_hess(B, t(V), t(up), t(tr), t(w), lam_f, t(lam), out)
-        assert ei.value.code == -4
-        return
     s.nlp_hess(B, t(V), t(up), t(tr), t(w), lam_f, t(lam), out)
     torch.cuda.synchronize()
     H = out.cpu().numpy()
