@@ -129,10 +129,12 @@ enum mmpc_hessian {
     MMPC_HESSIAN_EXACT = 2         /* + h sum_r lam_{k+1,r} d^2 f_r/d(x_k,u_k)^2 per stage (lam: the QP adjoint);
                                       an iteration whose KKT matrix is not positive definite on the null space takes
                                       the Gauss-Newton step.  Supported: nonlinear solves of models with second
-                                      derivatives on the RICCATI_GROUP solver (nx+nu < 16), unbounded or with control
-                                      bounds (the held controls are fixed in the exact QP; AUTO keeps Gauss-Newton
-                                      for bounded solves); state bounds and any other solve return
-                                      MMPC_ERR_UNSUPPORTED */
+                                      derivatives (the built-in 2-link arm and exo, SX-generated models) on the
+                                      RICCATI_GROUP solver (nx+nu < 16), unbounded or with control bounds (the held
+                                      controls are fixed in the exact QP; AUTO keeps Gauss-Newton for bounded
+                                      solves), and unbounded on the RICCATI (lane) solver; AUTO keeps Gauss-Newton
+                                      for the exo and on the lane solver.  State bounds, linear mode and any other
+                                      solve return MMPC_ERR_UNSUPPORTED */
 };
 
 typedef struct mmpc_opts {
