@@ -86,9 +86,6 @@ struct ExoArm {
     static constexpr int NX = 8;
     static constexpr int NU = 4;
     static constexpr int NQ = 4;  // second-order: x = [q; qd], xdot = [qd; acc(x, u)]
-    // acc = M^-1 (tau - D qd - G(q)) with constant diagonal D: d acc/d qd = -M^-1 D (JacPack stores 26 doubles)
-    static constexpr bool kMassDamped = true;
-    MMPC_HD static double damping(int j) { return exo::kDamping[j]; }
 
     // Cholesky of the upper-packed SPD matrix a (M00 M01 M02 M03 M11 M12 M13 M22 M23 M33):
     // l = lower factor packed (L00 L10 L11 L20 L21 L22 L30 L31 L32 L33), il = 1 / diag
@@ -291,82 +288,6 @@ struct ExoArm {
                 fu[(4 + r) * 4 + cc] = Fu[r * 4 + cc];
             }
         }
-    }
-};
-
-// Stage Jacobian as the lane kernel stores it (sqp_lane.h STORE_JAC): the h-scaled blocks hFq (NA x NQ), hFqd
-// (NA x NA), hFu (NA x NU) of A_k = I + h f_x, B_k = h f_u, written once per stage and iterate and read back by the
-// backward and step sweeps instead of re-evaluating the model there.  canon() brings a fresh evaluation to the form
-// pack/unpack reproduce bit for bit, so evaluated and stored Jacobians are the same numbers.
-// Generic models: the three blocks as they are.
-template <class M, class = void>
-struct JacPack {
-    static constexpr int NQ = M::NQ, NA = M::NX - M::NQ, NU = M::NU;
-    static constexpr int kSize = NA * NQ + NA * NA + NA * NU;
-    MMPC_HD static void canon(double*, double*, double*) {}
-    template <class P>
-    MMPC_HD static void pack(const double* hFq, const double* hFqd, const double* hFu, P* out) {
-#pragma unroll
-        for (int i = 0; i < NA * NQ; ++i) out[i * 64] = hFq[i];
-#pragma unroll
-        for (int i = 0; i < NA * NA; ++i) out[(NA * NQ + i) * 64] = hFqd[i];
-#pragma unroll
-        for (int i = 0; i < NA * NU; ++i) out[(NA * NQ + NA * NA + i) * 64] = hFu[i];
-    }
-    MMPC_HD static void unpack(const double* in, double* hFq, double* hFqd, double* hFu) {
-#pragma unroll
-        for (int i = 0; i < NA * NQ; ++i) hFq[i] = in[i];
-#pragma unroll
-        for (int i = 0; i < NA * NA; ++i) hFqd[i] = in[NA * NQ + i];
-#pragma unroll
-        for (int i = 0; i < NA * NU; ++i) hFu[i] = in[NA * NQ + NA * NA + i];
-    }
-};
-// Mass-matrix models with viscous damping and no velocity coupling (the exo: acc = M(q)^-1 (tau - D qd - G(q)),
-// Model::kMassDamped): d acc/d tau = M^-1 is symmetric and d acc/d qd = -M^-1 D, so hFu is stored as its upper
-// triangle and hFqd is rebuilt as -hFu D: 16 + 10 doubles per stage instead of 48.
-template <class M>
-struct JacPack<M, std::enable_if_t<M::kMassDamped>> {
-    static constexpr int NQ = M::NQ, NU = M::NU;
-    static_assert(M::NX == 2 * NQ && NU == NQ, "second-order, fully actuated");
-    static constexpr int kSize = NQ * NQ + NQ * (NQ + 1) / 2;
-    // upper triangle of hFu mirrored, hFqd = -hFu D
-    MMPC_HD static void canon(double* hFq, double* hFqd, double* hFu) {
-        (void)hFq;
-#pragma unroll
-        for (int i = 0; i < NQ; ++i)
-#pragma unroll
-            for (int j = 0; j < i; ++j) hFu[i * NQ + j] = hFu[j * NQ + i];
-#pragma unroll
-        for (int i = 0; i < NQ; ++i)
-#pragma unroll
-            for (int j = 0; j < NQ; ++j) hFqd[i * NQ + j] = -hFu[i * NQ + j] * M::damping(j);
-    }
-    template <class P>
-    MMPC_HD static void pack(const double* hFq, const double*, const double* hFu, P* out) {
-#pragma unroll
-        for (int i = 0; i < NQ * NQ; ++i) out[i * 64] = hFq[i];
-        int t = NQ * NQ;
-#pragma unroll
-        for (int i = 0; i < NQ; ++i)
-#pragma unroll
-            for (int j = i; j < NQ; ++j) out[(t++) * 64] = hFu[i * NQ + j];
-    }
-    MMPC_HD static void unpack(const double* in, double* hFq, double* hFqd, double* hFu) {
-#pragma unroll
-        for (int i = 0; i < NQ * NQ; ++i) hFq[i] = in[i];
-        int t = NQ * NQ;
-#pragma unroll
-        for (int i = 0; i < NQ; ++i)
-#pragma unroll
-            for (int j = i; j < NQ; ++j) {
-                hFu[i * NQ + j] = in[t];
-                hFu[j * NQ + i] = in[t++];
-            }
-#pragma unroll
-        for (int i = 0; i < NQ; ++i)
-#pragma unroll
-            for (int j = 0; j < NQ; ++j) hFqd[i * NQ + j] = -hFu[i * NQ + j] * M::damping(j);
     }
 };
 

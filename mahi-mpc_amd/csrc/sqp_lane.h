@@ -34,32 +34,25 @@ namespace mmpc {
 // the linear-mode data (one stage for the built-in models); the stage(s) after it are per-lane scratch for
 // the Riccati step (W = P_xx A).  A field block longer than a stage simply runs on into the next stage.
 // xb: the interior-point variant's per-stage z_l, z_u, Sigma, b, z_u - z_l of (x_{k+1} | u_k) replace the hold field
-// jp: doubles of the stored stage Jacobian (models.h JacPack; -1 = the generic size (nx - nq)(nx + nu), the largest)
-__host__ __device__ constexpr int lane_jac_doubles(int nx, int nu, int nq, int jp = -1) {
-    return jp >= 0 ? jp : (nx - nq) * (nx + nu);
-}
-__host__ __device__ constexpr int lane_stage_stride(int nx, int nu, int nq, bool xb = false, int jp = -1) {
-    return 5 * nx + 2 * nu + nu * (nx + nu + 1) + (xb ? 5 * (nx + nu) : 2 * nu + nx) + lane_jac_doubles(nx, nu, nq, jp);
+__host__ __device__ constexpr int lane_stage_stride(int nx, int nu, bool xb = false) {
+    return 5 * nx + 2 * nu + nu * (nx + nu + 1) + (xb ? 5 * (nx + nu) : 2 * nu + nx);
 }
 // linear-mode block: h-free Jacobian blocks da/dq (na x nq), da/dz (na x na), da/du (na x nu), xdot*, x*, u*
 __host__ __device__ constexpr int lane_lin_doubles(int nx, int nu, int nq) {
     return (nx - nq) * (nq + (nx - nq) + nu) + 2 * nx + nu;
 }
-__host__ __device__ constexpr int lane_lin_stages(int nx, int nu, int nq, bool xb = false, int jp = -1) {
-    return (lane_lin_doubles(nx, nu, nq) + lane_stage_stride(nx, nu, nq, xb, jp) - 1) /
-           lane_stage_stride(nx, nu, nq, xb, jp);
+__host__ __device__ constexpr int lane_lin_stages(int nx, int nu, int nq, bool xb = false) {
+    return (lane_lin_doubles(nx, nu, nq) + lane_stage_stride(nx, nu, xb) - 1) / lane_stage_stride(nx, nu, xb);
 }
 __host__ __device__ constexpr bool lane_w_in_lds(int nx, int nu, int nq);
-__host__ __device__ constexpr int lane_scratch_stages(int nx, int nu, int nq, bool xb = false, int jp = -1) {
-    return lane_w_in_lds(nx, nu, nq) ? 0
-                                     : (nx * nx + lane_stage_stride(nx, nu, nq, xb, jp) - 1) /
-                                           lane_stage_stride(nx, nu, nq, xb, jp);
+__host__ __device__ constexpr int lane_scratch_stages(int nx, int nu, int nq, bool xb = false) {
+    return lane_w_in_lds(nx, nu, nq) ? 0 : (nx * nx + lane_stage_stride(nx, nu, xb) - 1) / lane_stage_stride(nx, nu, xb);
 }
-__host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int nq, int N, bool xb = false, int jp = -1) {
-    return (N + 1 + lane_lin_stages(nx, nu, nq, xb, jp) + lane_scratch_stages(nx, nu, nq, xb, jp)) *
-           lane_stage_stride(nx, nu, nq, xb, jp);
+__host__ __device__ constexpr int lane_ws_doubles(int nx, int nu, int nq, int N, bool xb = false) {
+    return (N + 1 + lane_lin_stages(nx, nu, nq, xb) + lane_scratch_stages(nx, nu, nq, xb)) *
+           lane_stage_stride(nx, nu, xb);
 }
-template <int NX, int NU, int NQ, int JP, bool XB = false>
+template <int NX, int NU, bool XB = false>
 struct StageFields {
     static constexpr int NS = NX + NU;
     static constexpr int X = 0;             // x_k
@@ -77,10 +70,8 @@ struct StageFields {
     // interior point (XB, no hold field): y = (x_{k+1} | u_k) duals, Sigma, b, z_u - z_l
     static constexpr int NY = NX + NU;
     static constexpr int ZL = HOLD, ZU = ZL + NY, SG = ZU + NY, BB = SG + NY, ZG = BB + NY;
-    // the stage Jacobian (JacPack) at the iterate, written where it is evaluated (pass (1) or the alpha = 1 trial)
-    static constexpr int JAC = XB ? ZG + NY : U1 + NU;
-    static constexpr int SS = JAC + JP;
-    static_assert(SS == lane_stage_stride(NX, NU, NQ, XB, JP), "layout");
+    static constexpr int SS = XB ? ZG + NY : U1 + NU;
+    static_assert(SS == lane_stage_stride(NX, NU, XB), "layout");
 };
 
 struct LaneWork {
@@ -153,18 +144,6 @@ MMPC_HD void at_mul(T h, const T* hFq, const T* hFqd, const T* v, T* out) {
 // next stage's prefetches and all LDS traffic at each workspace access.
 template <class T>
 using gmem = __attribute__((address_space(1))) T;
-
-// A/B knobs of the stored-Jacobian change (round 4): which sweeps read the stored stage Jacobian instead of
-// evaluating the model, and where the backward sweep issues its one-stage-ahead loads
-#ifndef MMPC_LANE_JAC_BWD
-#define MMPC_LANE_JAC_BWD 1
-#endif
-#ifndef MMPC_LANE_JAC_STEP
-#define MMPC_LANE_JAC_STEP 1
-#endif
-#ifndef MMPC_LANE_PF_EARLY
-#define MMPC_LANE_PF_EARLY 0
-#endif
 __device__ __forceinline__ gmem<double>* stage_ptr(double* wsb, int64_t k, int SS, int lane) {
     gmem<double>* q = (gmem<double>*)(wsb + k * SS * 64 + lane);
     asm volatile("" : "+v"(q));
@@ -202,14 +181,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     const int N = p.N;
     const int NV = NX * (N + 1) + NU * N;
     const double h = p.h;
-    using JPK = JacPack<Model>;
-    constexpr int JP = JPK::kSize;
-    using SF = StageFields<NX, NU, NQ, JP, XB>;
+    using SF = StageFields<NX, NU, XB>;
     constexpr int NY = NX + NU;
     constexpr int SS = SF::SS;
     const int lane = threadIdx.x;
-    double* const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)lane_ws_doubles(NX, NU, NQ, N, XB, JP) * 64);  // wave-uniform
-    const int kScratch = N + 1 + lane_lin_stages(NX, NU, NQ, XB, JP);  // first stage of the W = P_xx A scratch
+    double* const wsb = lw.ws + (int64_t)blockIdx.x * ((int64_t)lane_ws_doubles(NX, NU, NQ, N, XB) * 64);  // wave-uniform
+    const int kScratch = N + 1 + lane_lin_stages(NX, NU, NQ, XB);  // first stage of the W = P_xx A scratch
     constexpr bool WLDS = lane_w_in_lds(NX, NU, NQ);  // W's a-rows in the dead P~ slots, no HBM scratch
 #define ST(k, f, e) wsb[((int64_t)(k) * SS + (f) + (e)) * 64 + lane]  // one-off accesses
 #define SK(dk, f, e) sk[((dk) * SS + (f) + (e)) * 64]                   // stage k + dk inside a stage loop
@@ -338,7 +315,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             _Pragma("unroll") for (int i_ = 0; i_ < NA * NQ; ++i_) hFq[i_] *= h;                         \
             _Pragma("unroll") for (int i_ = 0; i_ < NA * NA; ++i_) hFqd[i_] *= h;                        \
             _Pragma("unroll") for (int i_ = 0; i_ < NA * NU; ++i_) hFu[i_] *= h;                         \
-            JPK::canon(hFq, hFqd, hFu);                                                                  \
         }                                                                                                \
     } while (0)
 
@@ -397,7 +373,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                     rk[r] = SK(0, SF::R, r);
                 }
                 STAGE_EVAL(xk, u, xd, hFq, hFqd, hFu, true);
-                JPK::pack(hFq, hFqd, hFu, &SK(0, SF::JAC, 0));   // read back by (2) and (3)
                 double dn[NX];
                 a_mul<NQ, NA>(h, hFq, hFqd, d, dn);
 #pragma unroll
@@ -478,58 +453,46 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                     }
                     lmax = fmax(lmax, fabs(lam[r]));
                 }
-                // software pipeline: everything step k-1 reads -- x, u, c, d and the stored Jacobian of stage k-1 (written
-                // where the model was evaluated at this iterate: pass (1) or the previous step sweep's alpha = 1 trial),
-                // r_{k-2}, u_{k-2} -- is loaded in step k once K_k is stored, so the loads fly during the P~ update
-                // (issued at the top of the step they would be live, unused, across the whole Riccati step)
-                double xpf[NX], upf[NU], cpf[NX], dpf[NX], jpf[JP], rpf[NX], umpf[NU];
-                auto prefetch = [&](int k1) {   // stage k1's operands
-                    gmem<double>* const s1 = stage_ptr(wsb, k1, SS, lane);
+                // software pipeline as in (1): x_{k-1}, u_{k-1} (model inputs of the next step) are loaded during
+                // step k, everything else of step k before its model evaluation
+                double xpf[NX], upf[NU];
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) {
-                        xpf[r] = s1[(FX + r) * 64];
-                        cpf[r] = s1[(SF::C + r) * 64];
-                        dpf[r] = s1[(SF::D + r) * 64];
-                        rpf[r] = k1 >= 1 ? s1[(-SS + SF::R + r) * 64] : 0.0;
-                    }
+                for (int c = 0; c < NU; ++c) {
+                    unext[c] = 0.0;
+                    upf[c] = ST(N - 1, FU, c);
+                }
 #pragma unroll
-                    for (int c = 0; c < NU; ++c) {
-                        upf[c] = s1[(FU + c) * 64];
-                        umpf[c] = k1 >= 1 ? s1[(-SS + FU + c) * 64] : up[c];
-                    }
-                    if (MMPC_LANE_JAC_BWD) {
-#pragma unroll
-                        for (int i = 0; i < JP; ++i) jpf[i] = s1[(SF::JAC + i) * 64];
-                    }
-                };
-#pragma unroll
-                for (int c = 0; c < NU; ++c) unext[c] = 0.0;
-                prefetch(N - 1);
+                for (int r = 0; r < NX; ++r) xpf[r] = ST(N - 1, FX, r);
                 #pragma unroll 1
                 for (int k = N - 1; k >= 0; --k) {
                     gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
-                    double x[NX], u[NU], um[NU], cc[NX], dk[NX], rkm[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU],
-                        tg[NU];
+                    double x[NX], u[NU], um[NU], cc[NX], dk[NX], rkm[NX], xd[NX], hFq[SQ], hFqd[NA * NA],
+                        hFu[NA * NU], tg[NU];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         x[r] = xpf[r];
-                        cc[r] = cpf[r];
-                        dk[r] = dpf[r];
+                        cc[r] = SK(0, SF::C, r);
+                        dk[r] = SK(0, SF::D, r);
                     }
 #pragma unroll
-                    for (int c = 0; c < NU; ++c) {
-                        u[c] = upf[c];
-                        um[c] = umpf[c];
-                    }
+                    for (int c = 0; c < NU; ++c) u[c] = upf[c];
+                    if (k >= 1) {
 #pragma unroll
-                    for (int r = 0; r < NX; ++r) rkm[r] = rpf[r];
-                    if (MMPC_LANE_JAC_BWD) {
-                        JPK::unpack(jpf, hFq, hFqd, hFu);
+                        for (int r = 0; r < NX; ++r) {
+                            rkm[r] = SK(-1, SF::R, r);
+                            xpf[r] = SK(-1, FX, r);
+                        }
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) um[c] = SK(-1, FU, c);
                     } else {
-                        double xd[NX];
-                        STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) rkm[r] = 0.0;
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) um[c] = up[c];
                     }
-                    if (MMPC_LANE_PF_EARLY && k >= 1) prefetch(k - 1);
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) upf[c] = um[c];
+                    STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
                     // exact Hessian: W_k at (x_k, u_k) with lam_{k+1} (lam holds it until the adjoint step below)
                     constexpr int KZ = NX + NU;
                     double Wk[EXACT ? KZ * KZ : 1];
@@ -769,7 +732,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         }
                     }
                     if (k == 0) break;  // s_0 = 0: P~_0 is never used
-                    if (!MMPC_LANE_PF_EARLY) prefetch(k - 1);
                     // P~_k = blkdiag(A^T W + Q, R) - Y^T Y (old P is dead: overwrite it in place), p~_k = pn - Y^T yh
                     if constexpr (WLDS) {
                         // W in LDS: the a-rows of W (used by every output row) go to the dead P_xu / P_uu slots; the
@@ -939,7 +901,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 #pragma unroll 1
                 for (int k = 0; k < N; ++k) {
                     gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
-                    double x[NX], u[NU], rk[NX], ck[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU], dxk[NX], jk[JP];
+                    double x[NX], u[NU], xd[NX], rk[NX], ck[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU], dxk[NX];
 #pragma unroll
                     for (int r = 0; r < NX; ++r) dxk[r] = dx[r];
 #pragma unroll
@@ -948,10 +910,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         xpf[r] = SK(1, FX, r);
                         rk[r] = SK(0, SF::R, r);
                         ck[r] = SK(0, SF::C, r);
-                    }
-                    if (MMPC_LANE_JAC_STEP) {
-#pragma unroll
-                        for (int i = 0; i < JP; ++i) jk[i] = SK(0, SF::JAC, i);   // A_k, B_k at this iterate (stored)
                     }
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
@@ -1009,17 +967,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                             }
                         }
                     }
-                    double Fk[NX];
-                    if (MMPC_LANE_JAC_STEP) {
-                        JPK::unpack(jk, hFq, hFqd, hFu);
-#pragma unroll
-                        for (int r = 0; r < NX; ++r) Fk[r] = ck[r] + xpf[r];   // F_k = c_k + x_{k+1}
-                    } else {
-                        double xd[NX];
-                        STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
-#pragma unroll
-                        for (int r = 0; r < NX; ++r) Fk[r] = fma(h, xd[r], x[r]);
-                    }
+                    STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
                     double ad[NX];
                     a_mul<NQ, NA>(h, hFq, hFqd, dx, ad);
 #pragma unroll
@@ -1028,7 +976,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
-                        const double F = Fk[r];
+                        const double F = fma(h, xd[r], x[r]);
                         const double qe = 2.0 * Q[r] * (F - rk[r]);
                         dJ = fma(qe, ad[r], dJ);
                         dx[r] = ad[r] + ck[r];
@@ -1053,9 +1001,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         if constexpr (FUSE_FWD) {
                             double tFq[SQ], tFqd[NA * NA], tFu[NA * NU], dn[NX];
                             STAGE_EVAL(xt, ut, xdt, tFq, tFqd, tFu, true);
-                            // the next iteration's A_k, B_k (this stage's were read above); a rejected full step
-                            // re-evaluates them in (1)
-                            JPK::pack(tFq, tFqd, tFu, &SK(0, SF::JAC, 0));
                             a_mul<NQ, NA>(h, tFq, tFqd, dt, dn);
 #pragma unroll
                             for (int r = 0; r < NX; ++r) {

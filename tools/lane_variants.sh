@@ -11,15 +11,20 @@
 #   nolr      + -mllvm -amdgpu-opt-vgpr-liverange=0   (SIOptimizeVGPRLiveRange off: VGPR live ranges across
 #             divergent if/else and loop exits are not shortened)
 #   prealloc  + -mllvm -amdgpu-prealloc-sgpr-spill-vgprs (the VGPRs that hold spilled SGPR lanes reserved up front)
+#   sgprbasic / wwmbasic / vgprbasic
+#             + -mllvm -{sgpr,wwm,vgpr}-regalloc=basic (the basic instead of the greedy allocator for that register
+#             class: SGPRs, the whole-wave VGPRs that hold spilled SGPR lanes, ordinary VGPRs)
+# SRC: the tree whose csrc/ is patched (default: this one; e.g. a git worktree of the round-3 commit e022ea8)
 # Usage: tools/lane_variants.sh "shipped xbload unifw lup" "f0 nolr prealloc"   (builds in parallel, 4 at a time)
 set -o pipefail
 cd "$(dirname "$0")/.."
+SRC=${SRC:-$PWD}
 VARS=${1:-"shipped xbload unifw lup"}
 FLAGS=${2:-"f0 nolr prealloc"}
 BASE="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -mllvm -pragma-unroll-threshold=1000000"
 build() {
   local v=$1 f=$2 d=lib_var/${1}_${2}
-  rm -rf "$d" && mkdir -p "$d/csrc" "$d/include" && cp mahi-mpc_amd/csrc/* "$d/csrc/" && cp include/mmpc.h "$d/include/"
+  rm -rf "$d" && mkdir -p "$d/csrc" "$d/include" && cp "$SRC"/mahi-mpc_amd/csrc/* "$d/csrc/" && cp "$SRC"/include/mmpc.h "$d/include/"
   local L=$d/csrc/sqp_lane.h
   case $v in
     xbload) python3 - "$L" <<'EOF'
@@ -50,6 +55,9 @@ EOF
     f0) ;;
     nolr) extra="-mllvm -amdgpu-opt-vgpr-liverange=0";;
     prealloc) extra="-mllvm -amdgpu-prealloc-sgpr-spill-vgprs";;
+    sgprbasic) extra="-mllvm -sgpr-regalloc=basic";;
+    wwmbasic) extra="-mllvm -wwm-regalloc=basic";;
+    vgprbasic) extra="-mllvm -vgpr-regalloc=basic";;
     *) echo "unknown flags $f"; return 1;;
   esac
   # the copied mmpc.hip includes ../../include/mmpc.h relative to csrc: point it at the copy
