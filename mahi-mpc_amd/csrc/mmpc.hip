@@ -21,6 +21,7 @@
 
 #include "../../include/mmpc.h"
 #include "json_lite.h"
+#include "lane_launch.h"
 #include "models.h"
 #include "sqp_group.h"
 #include "sqp_lane.h"
@@ -660,20 +661,6 @@ int launch_group(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const So
     return MMPC_OK;
 }
 
-template <class Model, class FT>
-void launch_lane(bool bounded, bool xb, dim3 grid, dim3 block, hipStream_t stream, const SolveParams& p, LaneWork lw,
-                 bool exact = false) {
-    if constexpr (HasHess<Model>::value && std::is_same<FT, double>::value) {
-        if (exact && !bounded && !xb) {
-            sqp_lane_kernel<Model, double, false, false, true><<<grid, block, 0, stream>>>(p, lw);
-            return;
-        }
-    }
-    if (xb) sqp_lane_kernel<Model, FT, false, true><<<grid, block, 0, stream>>>(p, lw);
-    else if (bounded) sqp_lane_kernel<Model, FT, true><<<grid, block, 0, stream>>>(p, lw);
-    else sqp_lane_kernel<Model, FT, false><<<grid, block, 0, stream>>>(p, lw);
-}
-
 // Riccati workspace (sqp_lane.h / sqp_group.h layouts), grown on demand.  Growth is synchronous:
 // hipFree waits for the kernels still using the old buffer.
 int ensure_workspace_bytes(mmpc_handle* h, size_t bytes, double** out) {
@@ -808,14 +795,10 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         int rc = ensure_workspace(h, B, &lw);
         if (rc) return rc;
         dim3 grid(grid1d(B, 64)), block(64);
-        const bool f32 = h->opts.factor_fp32 != 0;
-        rc = with_model(mi.model_id, [&](auto* m) {
-            using M = std::remove_pointer_t<decltype(m)>;
-            if (f32) launch_lane<M, float>(bounded, p.x_bounded != 0, grid, block, stream, p, lw);
-            else launch_lane<M, double>(bounded, p.x_bounded != 0, grid, block, stream, p, lw, hess == MMPC_HESSIAN_EXACT);
-            return MMPC_OK;
-        });
-        if (rc) return rc;
+        // lane kernels: their own translation unit (lane_kernels.hip, lane_launch.h)
+        if (launch_lane_kernels(mi.model_id, h->opts.factor_fp32 != 0, bounded, p.x_bounded != 0,
+                                hess == MMPC_HESSIAN_EXACT, grid, block, stream, p, lw) != 0)
+            return fail(MMPC_ERR_UNSUPPORTED, "model not compiled into this library");
     }
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;

@@ -942,9 +942,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         }
                     } else {
                         // interior-point variant: loads at their uses.  The batched-load form above, compiled for
-                        // the exo interior-point instantiation (256 VGPR + 256 AGPR + ~950 B/lane of spills), gave
-                        // lane-dependent wrong steps on gfx950 (non-converged instances in test_gpu_xbounds) although
-                        // it computes the same sums; this form is the one verified against the oracle.
+                        // the exo interior-point instantiation with ROCm 7.2's greedy SGPR allocator, computed wrong
+                        // steps in every lane (a register-allocation defect, not the source: the same IR is right
+                        // with -mllvm -sgpr-regalloc=basic or -vgpr-regalloc=basic); this translation
+                        // unit is built with the basic SGPR allocator (lane_launch.h), and this form stays.
 #pragma unroll
                         for (int a = 0; a < NU; ++a) {
                             const int base = a * NS;
