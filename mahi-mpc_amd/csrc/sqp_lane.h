@@ -170,7 +170,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)
     static_assert(NQ >= 0 && NA >= NQ, "x = [q; z] with qdot = z[0:NQ]");
     const int64_t inst = blockIdx.x * (int64_t)64 + threadIdx.x;
-    const int lane0 = threadIdx.x;
+    [[maybe_unused]] const int lane0 = threadIdx.x;  // used by the phase-timing build
     MMPC_PHASE_DECL
     // Riccati matrix P~ (packed upper, NS(NS+1)/2 doubles per lane) lives in LDS, lane-interleaved
     // (conflict-free): holding it in registers next to the stage blocks and the factor spills to scratch.
