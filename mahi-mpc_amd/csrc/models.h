@@ -119,8 +119,9 @@ struct ExoArm {
 
     MMPC_HD static void eval(const double* x, const double* u, double* xd) {
         double s[4], c[4];
+        const trig_cptr TK = trig_table();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sincos(x[i], &s[i], &c[i]);
+        for (int i = 0; i < 4; ++i) sincos_fast(TK, x[i], &s[i], &c[i]);
         const exo::TrigPowers tp(c[1], c[2], c[3], s[1], s[2], s[3]);
         double Mu[10];
         exo::mass_upper(tp, Mu);
@@ -148,8 +149,9 @@ struct ExoArm {
     MMPC_HD static void eval_acc_jac(const double* x, const double* u, double* qdd, double* Fq, double* Fqd,
                                      double* Fu) {
         double s[4], c[4];
+        const trig_cptr TK = trig_table();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sincos(x[i], &s[i], &c[i]);
+        for (int i = 0; i < 4; ++i) sincos_fast(TK, x[i], &s[i], &c[i]);
         const exo::TrigPowers tp(c[1], c[2], c[3], s[1], s[2], s[3]);
         double Mu[10], l[10], il[4], w[4];
         exo::mass_upper(tp, Mu);
@@ -201,8 +203,9 @@ struct ExoArm {
     static constexpr bool kExactDefault = false;    // AUTO keeps Gauss-Newton: more iterations exact
     MMPC_HD static void eval_hess(const double* x, const double* u, const double* lam, double* W) {
         double s[4], c[4];
+        const trig_cptr TK = trig_table();
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sincos(x[i], &s[i], &c[i]);
+        for (int i = 0; i < 4; ++i) sincos_fast(TK, x[i], &s[i], &c[i]);
         const exo::TrigPowers tp(c[1], c[2], c[3], s[1], s[2], s[3]);
         double Mu[10], l[10], il[4], w[4], acc[4], mu[4];
         exo::mass_upper(tp, Mu);

@@ -9,6 +9,7 @@
 // Compiled for the device (models.h, TwoLinkArm) and for the host by the tests (oracle/builtin_hess_host.cpp), which
 // check it against the oracle's independent dual / hyper-dual restatement term by term of :36-37.
 #pragma once
+#include "fast_trig.h"
 
 namespace mmpc {
 
@@ -18,8 +19,9 @@ struct TwoLinkFast {
         double sA, cA, sB, cB, sAB, cAB, E, F, iD, nA, nB;
     };
     MMPC_HD static void terms(const double* x, const double* u, Terms& t) {
-        sincos(x[0], &t.sA, &t.cA);
-        sincos(x[1], &t.sB, &t.cB);
+        const trig_cptr TK = trig_table();
+        sincos_fast(TK, x[0], &t.sA, &t.cA);
+        sincos_fast(TK, x[1], &t.sB, &t.cB);
         t.cAB = fma(t.cA, t.cB, -t.sA * t.sB);
         t.sAB = fma(t.sA, t.cB, t.cA * t.sB);
         t.E = 1.0 + t.cB;
