@@ -1339,6 +1339,9 @@ int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) {
         unsigned long long z[16] = {0};
         MMPC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z)));
     }
+    unsigned long long lane[16];   // the lane kernels' table lives in their own translation unit (lane_launch.h)
+    MMPC_HIP(lane_phase_cycles(lane, reset != 0));
+    for (int i = 0; i < 16; ++i) out16[i] += lane[i];
     return MMPC_OK;
 }
 

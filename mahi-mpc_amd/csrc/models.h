@@ -75,6 +75,21 @@ struct IsControlAffine<M, std::enable_if_t<M::kControlAffine>> {
     static constexpr bool value = true;
 };
 
+// Directional derivative without the Jacobian (Model::eval_jvp): the lane kernel's step sweep only needs
+// A_k dx_k + B_k du_k and the trial's A d, not the blocks of A_k, B_k
+template <class M, class = void>
+struct HasJvp {
+    static constexpr bool value = false;
+};
+template <class M>
+struct HasJvp<M, std::enable_if_t<M::kHasJvp>> {
+    static constexpr bool value = true;
+};
+template <class M>
+MMPC_HD void model_jvp(const double* x, const double* u, const double* vx, const double* vu, double* xd, double* jv) {
+    if constexpr (HasJvp<M>::value) M::eval_jvp(x, u, vx, vu, xd, jv);   // callers test HasJvp first
+}
+
 // 4-DoF forearm/wrist exo, state [q0..q3, qd0..qd3] (util/testCorrectEquations.py:16-23),
 // control tau[4].  xdot = [qd; M(q)^-1 (tau - D qd - G(q))] with M(q) of src/inverseTest.cpp:59-74
 // (generated, exo_model_gen.h) and the build-defined gravity G_i = g_i sin q_i and viscous damping D of
@@ -88,22 +103,18 @@ struct ExoArm {
     static constexpr int NQ = 4;  // second-order: x = [q; qd], xdot = [qd; acc(x, u)]
 
     // Cholesky of the upper-packed SPD matrix a (M00 M01 M02 M03 M11 M12 M13 M22 M23 M33):
-    // l = lower factor packed (L00 L10 L11 L20 L21 L22 L30 L31 L32 L33), il = 1 / diag
+    // l = lower factor packed (L00 L10 L11 L20 L21 L22 L30 L31 L32 L33), il = 1 / diag (sqrt_rsqrt: no division)
     MMPC_HD static void chol4(const double* a, double* l, double* il) {
-        l[0] = sqrt(a[0]);
-        il[0] = 1.0 / l[0];
+        sqrt_rsqrt(a[0], l[0], il[0]);
         l[1] = a[1] * il[0];
         l[3] = a[2] * il[0];
         l[6] = a[3] * il[0];
-        l[2] = sqrt(a[4] - l[1] * l[1]);
-        il[1] = 1.0 / l[2];
+        sqrt_rsqrt(a[4] - l[1] * l[1], l[2], il[1]);
         l[4] = (a[5] - l[3] * l[1]) * il[1];
         l[7] = (a[6] - l[6] * l[1]) * il[1];
-        l[5] = sqrt(a[7] - l[3] * l[3] - l[4] * l[4]);
-        il[2] = 1.0 / l[5];
+        sqrt_rsqrt(a[7] - l[3] * l[3] - l[4] * l[4], l[5], il[2]);
         l[8] = (a[8] - l[6] * l[3] - l[7] * l[4]) * il[2];
-        l[9] = sqrt(a[9] - l[6] * l[6] - l[7] * l[7] - l[8] * l[8]);
-        il[3] = 1.0 / l[9];
+        sqrt_rsqrt(a[9] - l[6] * l[6] - l[7] * l[7] - l[8] * l[8], l[9], il[3]);
     }
     // y = (L L^T)^-1 b
     MMPC_HD static void chol4_solve(const double* l, const double* il, const double* b, double* y) {
@@ -189,6 +200,41 @@ struct ExoArm {
                 Fqd[r * 4 + j] = -Fu[r * 4 + j] * exo::kDamping[j];
             }
         }
+    }
+
+    // xd = f(x, u) and jv = d qdd / d(x, u) . (vq, vqd, vu) (vx = [vq; vqd]) without forming the Jacobian:
+    // differentiating M qdd = tau - D qd - G(q) along the direction, M jv = vu - D vqd - g cos(q) vq - sum_j vq_j (dM/dq_j) qdd
+    // (q0 does not enter M): one more Cholesky solve instead of M^-1's four, no 4x4x4 product, no h-scaled blocks
+    static constexpr bool kHasJvp = true;
+    MMPC_HD static void eval_jvp(const double* x, const double* u, const double* vx, const double* vu, double* xd,
+                                 double* jv) {
+        double s[4], c[4];
+        const trig_cptr TK = trig_table();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sincos_fast(TK, x[i], &s[i], &c[i]);
+        const exo::TrigPowers tp(c[1], c[2], c[3], s[1], s[2], s[3]);
+        double Mu[10], l[10], il[4], w[4];
+        exo::mass_upper(tp, Mu);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = u[i] - exo::kDamping[i] * x[4 + i] - exo::kGravityGain[i] * s[i];
+        chol4(Mu, l, il);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xd[i] = x[4 + i];
+        double* const qdd = xd + 4;
+        chol4_solve(l, il, w, qdd);
+        double r[4], t1[4], t2[4], t3[4];
+        dmass_times<1>(tp, qdd, t1);
+        dmass_times<2>(tp, qdd, t2);
+        dmass_times<3>(tp, qdd, t3);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            double t = fma(-exo::kDamping[i], vx[4 + i], vu[i]);
+            t = fma(-exo::kGravityGain[i] * c[i], vx[i], t);
+            t = fma(-vx[1], t1[i], t);
+            t = fma(-vx[2], t2[i], t);
+            r[i] = fma(-vx[3], t3[i], t);
+        }
+        chol4_solve(l, il, r, jv);
     }
 
     // W = sum_s lam[s] d^2 acc_s / d(x, u)^2 (12 x 12 row-major over z = (q, qd, tau)): the dynamics part of the

@@ -136,6 +136,15 @@ MMPC_HD void at_mul(T h, const T* hFq, const T* hFqd, const T* v, T* out) {
     }
 }
 
+// A v (+ B w) from the directional derivative jv = da/d(x, u) . (v, w): [v_q + h v_z[0:NQ]; v_z + h jv]
+template <int NQ, int NA>
+MMPC_HD void jvp_step(double h, const double* v, const double* jv, double* out) {
+#pragma unroll
+    for (int i = 0; i < NQ; ++i) out[i] = fma(h, v[NQ + i], v[i]);
+#pragma unroll
+    for (int i = 0; i < NA; ++i) out[NQ + i] = fma(h, jv[i], v[NQ + i]);
+}
+
 // Per-lane pointer to stage k of the workspace, opaque to the optimiser: every access of a stage loop is
 // derived from it (offset folded into the instruction or one add), so nothing is hoisted out of the loop.
 // Without it LICM materialises one 64-bit offset per (field, element) before the loop and spills them.
@@ -322,6 +331,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     int it = 0;
     double kkt = 0.0, mu = 0.0, pg_prev = INFINITY;
     constexpr bool FUSE_TRIAL = !BOUNDED && !XB;  // the alpha = 1 trial is evaluated inside the step sweep
+    // the forward and step sweeps need only A d and A dx + B du: a model with a directional derivative (ExoArm)
+    // evaluates that instead of the Jacobian blocks (linear mode keeps its stored blocks)
+    constexpr bool JVP = HasJvp<Model>::value;
     // FUSE_FWD (fp64 factor): the step sweep evaluates the alpha = 1 trial point with its Jacobian and forms there
     // everything pass (1) of the next iteration computes at that point (defects, d, J, |c|_1, max|c|), so when the
     // full step is accepted (99.7 % of the cfg#3 iterations, every one after the first: tools/alpha_stats.py) the
@@ -372,9 +384,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                     xn[r] = SK(1, FX, r);
                     rk[r] = SK(0, SF::R, r);
                 }
-                STAGE_EVAL(xk, u, xd, hFq, hFqd, hFu, true);
-                double dn[NX];
-                a_mul<NQ, NA>(h, hFq, hFqd, d, dn);
+                double dn[NX];   // A_k d_k
+                if (JVP && !lin) {
+                    double zu[NU], jv[NA];
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) zu[c] = 0.0;
+                    model_jvp<Model>(xk, u, d, zu, xd, jv);
+                    jvp_step<NQ, NA>(h, d, jv, dn);
+                } else {
+                    STAGE_EVAL(xk, u, xd, hFq, hFqd, hFu, true);
+                    a_mul<NQ, NA>(h, hFq, hFqd, d, dn);
+                }
 #pragma unroll
                 for (int r = 0; r < NX; ++r) {
                     const double F = fma(h, xd[r], xk[r]);
@@ -679,9 +699,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                         for (int q = 0; q < a; ++q) s = fma(-Ld[a][q], Ld[a][q], s);
                         fact_ok &= (s > (FT)0) && isfinite(s);
-                        const FT lj = sqrt(fmax(s, std::numeric_limits<FT>::min()));
-                        Ld[a][a] = lj;
-                        il[a] = (FT)1 / lj;
+                        if constexpr (std::is_same<FT, double>::value) {   // no sqrt + division sequences (device.h)
+                            sqrt_rsqrt(fmax(s, std::numeric_limits<FT>::min()), Ld[a][a], il[a]);
+                        } else {
+                            const FT lj = sqrt(fmax(s, std::numeric_limits<FT>::min()));
+                            Ld[a][a] = lj;
+                            il[a] = (FT)1 / lj;
+                        }
 #pragma unroll
                         for (int b = a + 1; b < NU; ++b) {
                             FT t = Hww[a][b];
@@ -702,7 +726,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                         double t = yh[a];
 #pragma unroll
                         for (int q = 0; q < a; ++q) t = fma(-(double)Ld[a][q], yh[q], t);
-                        yh[a] = t / (double)Ld[a][a];
+                        yh[a] = std::is_same<FT, double>::value ? t * (double)il[a] : t / (double)Ld[a][a];
                     }
                     // [K_k | kff_k] = -L^-T [Y | yh]: kff (fp64) in the first NU slots of the K field, K (FT) after it
                     {
@@ -720,7 +744,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                             double t = yh[a];
 #pragma unroll
                             for (int q = a + 1; q < NU; ++q) t = fma(-(double)Ld[q][a], kh[q], t);
-                            kh[a] = t / (double)Ld[a][a];
+                            kh[a] = std::is_same<FT, double>::value ? t * (double)il[a] : t / (double)Ld[a][a];
                         }
                         gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
                         gmem<FT>* const kk = (gmem<FT>*)(kb + NU * 64) + lane;
@@ -968,13 +992,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                             }
                         }
                     }
-                    STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
-                    double ad[NX];
-                    a_mul<NQ, NA>(h, hFq, hFqd, dx, ad);
+                    double ad[NX];   // A_k dx_k + B_k du_k
+                    if (JVP && !lin) {
+                        double jv[NA];
+                        model_jvp<Model>(x, u, dx, du, xd, jv);
+                        jvp_step<NQ, NA>(h, dx, jv, ad);
+                    } else {
+                        STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                        a_mul<NQ, NA>(h, hFq, hFqd, dx, ad);
 #pragma unroll
-                    for (int s = 0; s < NA; ++s)
+                        for (int s = 0; s < NA; ++s)
 #pragma unroll
-                        for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
+                            for (int c = 0; c < NU; ++c) ad[NQ + s] = fma(hFu[s * NU + c], du[c], ad[NQ + s]);
+                    }
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         const double F = fma(h, xd[r], x[r]);
@@ -1000,9 +1030,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #pragma unroll
                         for (int c = 0; c < NU; ++c) ut[c] = u[c] + du[c];
                         if constexpr (FUSE_FWD) {
-                            double tFq[SQ], tFqd[NA * NA], tFu[NA * NU], dn[NX];
-                            STAGE_EVAL(xt, ut, xdt, tFq, tFqd, tFu, true);
-                            a_mul<NQ, NA>(h, tFq, tFqd, dt, dn);
+                            double dn[NX];   // A d at the trial point, as pass (1)
+                            if (JVP && !lin) {
+                                double zu[NU], jv[NA];
+#pragma unroll
+                                for (int c = 0; c < NU; ++c) zu[c] = 0.0;
+                                model_jvp<Model>(xt, ut, dt, zu, xdt, jv);
+                                jvp_step<NQ, NA>(h, dt, jv, dn);
+                            } else {
+                                double tFq[SQ], tFqd[NA * NA], tFu[NA * NU];
+                                STAGE_EVAL(xt, ut, xdt, tFq, tFqd, tFu, true);
+                                a_mul<NQ, NA>(h, tFq, tFqd, dt, dn);
+                            }
 #pragma unroll
                             for (int r = 0; r < NX; ++r) {
                                 const double F = fma(h, xdt[r], xt[r]);
