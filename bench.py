@@ -626,9 +626,9 @@ def model_flops_per_iteration(mmpc, cfg, ksolver, N, hess):
     x the evaluations per stage the kernel runs per iteration:
       16-lane kernel (sqp_group.h): the alpha = 1 trial with its Jacobian (phase A's data for the next iteration), and
         with the exact Hessian the stage Hessian W_k;
-      lane kernel (sqp_lane.h), fp64 factor: Jacobians in the backward sweep, at (x_k, u_k) in the step sweep and at
-        the full-step point (the next forward pass); fp32 factor: forward, backward and step Jacobians + the value-only
-        alpha = 1 trial.
+      lane kernel (sqp_lane.h): the Jacobian in the backward sweep; A dx + B du at (x_k, u_k) in the step sweep and
+        A d at the full-step point (the next forward pass) -- directional derivatives for a model that has them (the
+        exo: acc_jac_h + 2 jvp), Jacobians otherwise (3 acc_jac).
     The first iteration's initial evaluation and any alpha < 1 trial are not counted (a lower bound)."""
     try:
         tab = json.load(open(os.path.join(os.path.dirname(mmpc.__file__), "model_flops.json")))["models"]
@@ -640,7 +640,7 @@ def model_flops_per_iteration(mmpc, cfg, ksolver, N, hess):
     if ksolver == 3:
         ev = {"acc_jac": 1, "hess": 1 if hess == mmpc.HESSIAN_EXACT else 0}
     elif ksolver == 2:
-        ev = {"acc_jac": 3, "eval": 1} if cfg["fp32"] else {"acc_jac": 3}
+        ev = {"acc_jac_h": 1, "jvp": 2} if "jvp" in model else {"acc_jac": 3}
     else:
         return None
     ev = {k: v for k, v in ev.items() if v}

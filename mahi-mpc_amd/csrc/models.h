@@ -85,6 +85,20 @@ template <class M>
 struct HasJvp<M, std::enable_if_t<M::kHasJvp>> {
     static constexpr bool value = true;
 };
+// Jacobian blocks already scaled by the step h (Model::eval_acc_jac_h)
+template <class M, class = void>
+struct HasJacH {
+    static constexpr bool value = false;
+};
+template <class M>
+struct HasJacH<M, std::enable_if_t<M::kHasJacH>> {
+    static constexpr bool value = true;
+};
+template <class M>
+MMPC_HD void model_acc_jac_h(const double* x, const double* u, double h, double* acc, double* hFq, double* hFqd,
+                             double* hFu) {
+    if constexpr (HasJacH<M>::value) M::eval_acc_jac_h(x, u, h, acc, hFq, hFqd, hFu);   // callers test HasJacH first
+}
 template <class M>
 MMPC_HD void model_jvp(const double* x, const double* u, const double* vx, const double* vu, double* xd, double* jv) {
     if constexpr (HasJvp<M>::value) M::eval_jvp(x, u, vx, vu, xd, jv);   // callers test HasJvp first
@@ -235,6 +249,75 @@ struct ExoArm {
             r[i] = fma(-vx[3], t3[i], t);
         }
         chol4_solve(l, il, r, jv);
+    }
+
+    // eval_acc_jac with the blocks already scaled by h (hFq = h d qdd/dq, hFqd, hFu), the form the Riccati kernels
+    // use: M^-1 = L^-T L^-1 from the inverse Cholesky factor (no solves against unit vectors, whose zeros are not
+    // folded) with h folded into one factor (no scaling pass over the 48 entries)
+    static constexpr bool kHasJacH = true;
+    MMPC_HD static void eval_acc_jac_h(const double* x, const double* u, double h, double* qdd, double* hFq,
+                                       double* hFqd, double* hFu) {
+        double s[4], c[4];
+        const trig_cptr TK = trig_table();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sincos_fast(TK, x[i], &s[i], &c[i]);
+        const exo::TrigPowers tp(c[1], c[2], c[3], s[1], s[2], s[3]);
+        double Mu[10], l[10], il[4], w[4];
+        exo::mass_upper(tp, Mu);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = u[i] - exo::kDamping[i] * x[4 + i] - exo::kGravityGain[i] * s[i];
+        chol4(Mu, l, il);
+        chol4_solve(l, il, w, qdd);
+        // Li = L^-1 (lower), l packed as chol4's L00 L10 L11 L20 L21 L22 L30 L31 L32 L33
+        double Li[4][4];
+        Li[0][0] = il[0];
+        Li[1][1] = il[1];
+        Li[2][2] = il[2];
+        Li[3][3] = il[3];
+        Li[1][0] = -(l[1] * Li[0][0]) * il[1];
+        Li[2][1] = -(l[4] * Li[1][1]) * il[2];
+        Li[2][0] = -fma(l[3], Li[0][0], l[4] * Li[1][0]) * il[2];
+        Li[3][2] = -(l[8] * Li[2][2]) * il[3];
+        Li[3][1] = -fma(l[7], Li[1][1], l[8] * Li[2][1]) * il[3];
+        Li[3][0] = -fma(l[6], Li[0][0], fma(l[7], Li[1][0], l[8] * Li[2][0])) * il[3];
+        // h M^-1 = Li^T (h Li): entry (i, j) sums over the rows k >= max(i, j)
+        double hLi[4][4], hMi[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j <= k; ++j) hLi[k][j] = h * Li[k][j];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = i; j < 4; ++j) {
+                double t = Li[j][i] * hLi[j][j];
+#pragma unroll
+                for (int k = j + 1; k < 4; ++k) t = fma(Li[k][i], hLi[k][j], t);
+                hMi[i][j] = t;
+                hMi[j][i] = t;
+            }
+        // h d qdd/dq_j = h M^-1 (-(dM/dq_j) qdd - g_j cos q_j e_j) (dM/dq_0 = 0);  h d qdd/dqd_j = -h M^-1 e_j D_j
+        double t1[4], t2[4], t3[4];
+        dmass_times<1>(tp, qdd, t1);
+        dmass_times<2>(tp, qdd, t2);
+        dmass_times<3>(tp, qdd, t3);
+        const double* const tj[4] = {nullptr, t1, t2, t3};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            hFq[r * 4] = hMi[r][0] * (-exo::kGravityGain[0] * c[0]);
+#pragma unroll
+            for (int j = 1; j < 4; ++j) {
+                double t = hMi[r][j] * (-exo::kGravityGain[j] * c[j]);
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) t = fma(-hMi[r][cc], tj[j][cc], t);
+                hFq[r * 4 + j] = t;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                hFu[r * 4 + j] = hMi[r][j];
+                hFqd[r * 4 + j] = -hMi[r][j] * exo::kDamping[j];
+            }
+        }
     }
 
     // W = sum_s lam[s] d^2 acc_s / d(x, u)^2 (12 x 12 row-major over z = (q, qd, tau)): the dynamics part of the

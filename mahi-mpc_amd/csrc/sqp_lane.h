@@ -25,6 +25,20 @@
 #include "models.h"
 #include "sqp_wave.h"
 
+// A/B switches of the fp32-factor instantiations (diagnostic builds only; defaults are the shipped choice)
+#ifndef MMPC_LANE_YLO32
+#define MMPC_LANE_YLO32 1
+#endif
+#ifndef MMPC_LANE_JACH32
+#define MMPC_LANE_JACH32 1
+#endif
+#ifndef MMPC_LANE_LB32
+#define MMPC_LANE_LB32 1
+#endif
+#ifndef MMPC_LANE_FWD32
+#define MMPC_LANE_FWD32 0
+#endif
+
 namespace mmpc {
 
 // Workspace layout, stage-major: [64-instance block][stage k = 0..N+1][field][lane].  All fields of
@@ -218,16 +232,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     double lbv[NU], ubv[NU];
     load_bounds<NU, BOUNDED>(p, lbv, ubv);
     // ---- load: V (reference layout) -> SoA X/U, x_0 pinned (ModelControl.cpp:144-145), targets ----
+    // Every copy below loads LB stages into registers before storing them: the workspace stores may alias the input
+    // pointers, so a load-store-load order would wait out one memory round trip per element (the load and
+    // write-back phases took 9.5 % of the cfg#3 kernel that way).
+    constexpr int LB = (std::is_same<FT, double>::value || MMPC_LANE_LB32) ? 5 : 1;
     {
         const double* Vin = p.V + inst * (int64_t)NV;
-        for (int k = 0; k < N; ++k) {
+        double x0v[NX];
 #pragma unroll
-            for (int r = 0; r < NX; ++r)
-                ST(k, FX, r) = (k == 0 || p.init_hold) ? p.x0[inst * NX + r] : (p.init_zero ? 0.0 : Vin[k * ND + r]);
+        for (int r = 0; r < NX; ++r) x0v[r] = p.x0[inst * NX + r];
+        for (int k0 = 0; k0 < N; k0 += LB) {
+            double v[LB][ND];
 #pragma unroll
-            for (int c = 0; c < NU; ++c) {
-                const double v = p.init_zero ? 0.0 : Vin[k * ND + NX + c];
-                ST(k, FU, c) = BOUNDED ? proj(v, lbv[c], ubv[c]) : v;
+            for (int j = 0; j < LB; ++j)
+#pragma unroll
+                for (int e = 0; e < ND; ++e) v[j][e] = (p.init_zero || k0 + j >= N) ? 0.0 : Vin[(k0 + j) * ND + e];
+#pragma unroll
+            for (int j = 0; j < LB; ++j) {
+                const int k = k0 + j;
+                if (k < N) {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) ST(k, FX, r) = (k == 0 || p.init_hold) ? x0v[r] : v[j][r];
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) ST(k, FU, c) = BOUNDED ? proj(v[j][NX + c], lbv[c], ubv[c]) : v[j][NX + c];
+                }
             }
         }
 #pragma unroll
@@ -238,9 +266,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
             for (int r = 0; r < NX; ++r) ST(0, FXo, r) = p.x0[inst * NX + r];
         }
         const double* tr = p.traj + inst * (int64_t)N * NX;
-        for (int k = 0; k < N; ++k)
+        for (int k0 = 0; k0 < N; k0 += LB) {
+            double t[LB][NX];
 #pragma unroll
-            for (int r = 0; r < NX; ++r) ST(k, SF::R, r) = tr[k * NX + r];
+            for (int j = 0; j < LB; ++j)
+#pragma unroll
+                for (int r = 0; r < NX; ++r) t[j][r] = k0 + j < N ? tr[(k0 + j) * NX + r] : 0.0;
+#pragma unroll
+            for (int j = 0; j < LB; ++j)
+                if (k0 + j < N)
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) ST(k0 + j, SF::R, r) = t[j][r];
+        }
     }
     double yl[XB ? NY : 1], yu[XB ? NY : 1];
     double mub = kIpMu0;  // barrier parameter (f = J/2 scale)
@@ -286,7 +323,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
 #define STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, jac)                                                        \
     do {                                                                                                 \
         if (!lin) {                                                                                      \
-            if (jac) {                                                                                   \
+            if (jac && JACH) {   /* blocks come scaled: no pass below */                                   \
+                model_acc_jac_h<Model>(x, u, h, xd + NQ, hFq, hFqd, hFu);                                \
+                _Pragma("unroll") for (int i_ = 0; i_ < NQ; ++i_) xd[i_] = x[NQ + i_];                   \
+            } else if (jac) {                                                                            \
                 Model::eval_acc_jac(x, u, xd + NQ, hFq, hFqd, hFu);                                      \
                 _Pragma("unroll") for (int i_ = 0; i_ < NQ; ++i_) xd[i_] = x[NQ + i_];                   \
             } else {                                                                                     \
@@ -320,7 +360,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                 xd[NQ + i_] = t_;                                                                        \
             }                                                                                            \
         }                                                                                                \
-        if (jac) {                                                                                       \
+        if (jac && (lin || !JACH)) {                                                                             \
             _Pragma("unroll") for (int i_ = 0; i_ < NA * NQ; ++i_) hFq[i_] *= h;                         \
             _Pragma("unroll") for (int i_ = 0; i_ < NA * NA; ++i_) hFqd[i_] *= h;                        \
             _Pragma("unroll") for (int i_ = 0; i_ < NA * NU; ++i_) hFu[i_] *= h;                         \
@@ -334,13 +374,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     // the forward and step sweeps need only A d and A dx + B du: a model with a directional derivative (ExoArm)
     // evaluates that instead of the Jacobian blocks (linear mode keeps its stored blocks)
     constexpr bool JVP = HasJvp<Model>::value;
+    constexpr bool F64 = std::is_same<FT, double>::value;
+    // first row q of Y = L^-1 [H_wx | -R] that can be nonzero in column j (the -R block is lower triangular)
+    auto ylo = [](int j) constexpr { return (j < NX || !(F64 || MMPC_LANE_YLO32)) ? 0 : j - NX; };
+    constexpr bool JACH = HasJacH<Model>::value && (F64 || MMPC_LANE_JACH32);
     // FUSE_FWD (fp64 factor): the step sweep evaluates the alpha = 1 trial point with its Jacobian and forms there
     // everything pass (1) of the next iteration computes at that point (defects, d, J, |c|_1, max|c|), so when the
     // full step is accepted (99.7 % of the cfg#3 iterations, every one after the first: tools/alpha_stats.py) the
     // next iteration starts at (2).  This saves the value-only trial evaluation and pass (1)'s sweep (cfg#3:
     // 11.63 -> 11.20 ms); the fp32-factor build (cfg#5) spills more with it (10.05 -> 11.77 ms) and keeps the
     // separate pass.  fwd_ready: C and D of the workspace hold the accepted iterate's values.
-    constexpr bool FUSE_FWD = FUSE_TRIAL && std::is_same<FT, double>::value;
+    constexpr bool FUSE_FWD = FUSE_TRIAL && (std::is_same<FT, double>::value || MMPC_LANE_FWD32);
     bool fwd_ready = false;
     double J0n = 0.0, c1n = 0.0, cmaxn = 0.0;
     bool nfn = false;
@@ -718,9 +762,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                     for (int a = 0; a < NU; ++a) {
 #pragma unroll
                         for (int j = 0; j < NS; ++j) {
+                            // the -R columns stay lower triangular (L^-1 (-R), R diagonal): Y[q][NX + c] = 0 for q < c.
+                            // Multiplications by those zeros are not folded (0 * x is not 0 for x = inf / NaN), so
+                            // every loop over q below starts at the first row that can be nonzero (ylo)
+                            if (j >= NX && j - NX > a) {
+                                Y[a][j] = (FT)0;
+                                continue;
+                            }
                             FT t = Y[a][j];
 #pragma unroll
-                            for (int q = 0; q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
+                            for (int q = ylo(j); q < a; ++q) t = fma(-Ld[a][q], Y[q][j], t);
                             Y[a][j] = t * il[a];
                         }
                         double t = yh[a];
@@ -832,14 +883,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                     for (int a = 0; a < NS; ++a) {
                         double t = pn[a];
 #pragma unroll
-                        for (int q = 0; q < NU; ++q) t = fma(-(double)Y[q][a], yh[q], t);
+                        for (int q = ylo(a); q < NU; ++q) t = fma(-(double)Y[q][a], yh[q], t);
                         if (BOUNDED) t += pex[a];
                         pv[a] = t;
 #pragma unroll
                         for (int b = (a < NX ? NX : a); b < NS; ++b) {
                             FT v = (FT)((a == b) ? R[a - NX] : 0.0);
 #pragma unroll
-                            for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
+                            for (int q = ylo(b); q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);   // b >= a: ylo(b) >= ylo(a)
                             PS(a, b) = v;
                         }
                     }
@@ -1239,11 +1290,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     MMPC_PHASE(6);
     // ---- write back V (reference layout) ----
     double* Vout = p.V + inst * (int64_t)NV;
-    for (int k = 0; k < N; ++k) {
+    for (int k0 = 0; k0 < N; k0 += LB) {   // LB stages loaded before they are stored (see the load phase)
+        double v[LB][ND];
 #pragma unroll
-        for (int r = 0; r < NX; ++r) Vout[k * ND + r] = ST(k, FX, r);
+        for (int j = 0; j < LB; ++j) {
+            const int k = k0 + j < N ? k0 + j : N - 1;
 #pragma unroll
-        for (int c = 0; c < NU; ++c) Vout[k * ND + NX + c] = ST(k, FU, c);
+            for (int r = 0; r < NX; ++r) v[j][r] = ST(k, FX, r);
+#pragma unroll
+            for (int c = 0; c < NU; ++c) v[j][NX + c] = ST(k, FU, c);
+        }
+#pragma unroll
+        for (int j = 0; j < LB; ++j)
+            if (k0 + j < N)
+#pragma unroll
+                for (int e = 0; e < ND; ++e) Vout[(k0 + j) * ND + e] = v[j][e];
     }
 #pragma unroll
     for (int r = 0; r < NX; ++r) Vout[N * ND + r] = ST(N, FX, r);

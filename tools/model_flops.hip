@@ -15,6 +15,9 @@ __device__ inline void mmpc_flops_sincos(double x, double* s, double* c) {
     *c = b;
 }
 #define sincos(x, s, c) mmpc_flops_sincos(x, s, c)
+// the models call sincos_fast (fast_trig.h): define it first, then route the models' calls to the stub
+#include "../mahi-mpc_amd/csrc/fast_trig.h"
+#define sincos_fast(K, x, s, c) mmpc_flops_sincos(x, s, c)
 #include "../mahi-mpc_amd/csrc/models.h"
 
 using namespace mmpc;
@@ -48,6 +51,25 @@ __device__ void load(const double* in, double* x, double* u) {
 
 MODEL_KERNELS(TwoLinkArm)
 MODEL_KERNELS(ExoArm)
+
+// the lane kernel's exo evaluations: h-scaled Jacobian (backward sweep) and directional derivative (forward / step)
+extern "C" __global__ void flops_acc_jac_h_ExoArm(const double* in, double* out) {
+    double x[8], u[4], acc[4], Fq[16], Fqd[16], Fu[16];
+    load<ExoArm>(in, x, u);
+    ExoArm::eval_acc_jac_h(x, u, in[12], acc, Fq, Fqd, Fu);
+    int o = 0;
+    for (int i = 0; i < 4; ++i) out[o++] = acc[i];
+    for (int i = 0; i < 16; ++i) out[o++] = Fq[i];
+    for (int i = 0; i < 16; ++i) out[o++] = Fqd[i];
+    for (int i = 0; i < 16; ++i) out[o++] = Fu[i];
+}
+extern "C" __global__ void flops_jvp_ExoArm(const double* in, double* out) {
+    double x[8], u[4], xd[8], jv[4];
+    load<ExoArm>(in, x, u);
+    ExoArm::eval_jvp(x, u, in + 12, in + 20, xd, jv);
+    for (int i = 0; i < 8; ++i) out[i] = xd[i];
+    for (int i = 0; i < 4; ++i) out[8 + i] = jv[i];
+}
 
 extern "C" __global__ void flops_hess_TwoLinkArm(const double* in, double* out) {
     constexpr int NZ = TwoLinkArm::NX + TwoLinkArm::NU;
