@@ -21,6 +21,7 @@
 
 #include "../../include/mmpc.h"
 #include "json_lite.h"
+#include "group_launch.h"
 #include "lane_launch.h"
 #include "models.h"
 #include "sqp_group.h"
@@ -754,14 +755,21 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         if (hess < 0) return hess;
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
-            if constexpr (exact_capable<M>()) {
-                if (hess == MMPC_HESSIAN_EXACT)
-                    return bounded ? launch_group<M, true, false, true>(grid, block, lds, stream, p, gwk)
-                                   : launch_group<M, false, false, true>(grid, block, lds, stream, p, gwk);
+            if constexpr (std::is_same<M, TwoLinkArm>::value) {   // greedy-allocator unit (group_launch.h)
+                const hipError_t e = launch_group_two_link(bounded, xb, hess == MMPC_HESSIAN_EXACT, grid, block, lds,
+                                                           stream, p, gwk);
+                return e == hipSuccess ? MMPC_OK : fail(MMPC_ERR_HIP, std::string("group kernel launch: ") +
+                                                                          hipGetErrorString(e));
+            } else {
+                if constexpr (exact_capable<M>()) {
+                    if (hess == MMPC_HESSIAN_EXACT)
+                        return bounded ? launch_group<M, true, false, true>(grid, block, lds, stream, p, gwk)
+                                       : launch_group<M, false, false, true>(grid, block, lds, stream, p, gwk);
+                }
+                if (xb) return launch_group<M, false, true>(grid, block, lds, stream, p, gwk);
+                return bounded ? launch_group<M, true>(grid, block, lds, stream, p, gwk)
+                               : launch_group<M, false>(grid, block, lds, stream, p, gwk);
             }
-            if (xb) return launch_group<M, false, true>(grid, block, lds, stream, p, gwk);
-            return bounded ? launch_group<M, true>(grid, block, lds, stream, p, gwk)
-                           : launch_group<M, false>(grid, block, lds, stream, p, gwk);
         });
         if (rc) return rc;
         MMPC_HIP(hipGetLastError());
@@ -1342,6 +1350,10 @@ int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) {
     unsigned long long lane[16];   // the lane kernels' table lives in their own translation unit (lane_launch.h)
     MMPC_HIP(lane_phase_cycles(lane, reset != 0));
     for (int i = 0; i < 16; ++i) out16[i] += lane[i];
+#if MMPC_BUILTIN_MODELS
+    MMPC_HIP(group_two_link_phase_cycles(lane, reset != 0));   // the 2-link group kernels' unit (group_launch.h)
+    for (int i = 0; i < 16; ++i) out16[i] += lane[i];
+#endif
     return MMPC_OK;
 }
 

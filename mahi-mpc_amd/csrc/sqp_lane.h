@@ -244,9 +244,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int k0 = 0; k0 < N; k0 += LB) {
             double v[LB][ND];
 #pragma unroll
-            for (int j = 0; j < LB; ++j)
+            for (int j = 0; j < LB; ++j) {   // one uniform branch per stage, not per element
+                if (!p.init_zero && k0 + j < N) {
 #pragma unroll
-                for (int e = 0; e < ND; ++e) v[j][e] = (p.init_zero || k0 + j >= N) ? 0.0 : Vin[(k0 + j) * ND + e];
+                    for (int e = 0; e < ND; ++e) v[j][e] = Vin[(k0 + j) * ND + e];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < ND; ++e) v[j][e] = 0.0;
+                }
+            }
 #pragma unroll
             for (int j = 0; j < LB; ++j) {
                 const int k = k0 + j;
@@ -269,9 +275,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         for (int k0 = 0; k0 < N; k0 += LB) {
             double t[LB][NX];
 #pragma unroll
-            for (int j = 0; j < LB; ++j)
+            for (int j = 0; j < LB; ++j) {
+                const int kj = k0 + j < N ? k0 + j : N - 1;   // past the end: stage N-1 again, not stored
 #pragma unroll
-                for (int r = 0; r < NX; ++r) t[j][r] = k0 + j < N ? tr[(k0 + j) * NX + r] : 0.0;
+                for (int r = 0; r < NX; ++r) t[j][r] = tr[kj * NX + r];
+            }
 #pragma unroll
             for (int j = 0; j < LB; ++j)
                 if (k0 + j < N)
