@@ -36,7 +36,7 @@
 #define MMPC_LANE_LB32 1
 #endif
 #ifndef MMPC_LANE_FWD32
-#define MMPC_LANE_FWD32 0
+#define MMPC_LANE_FWD32 1
 #endif
 
 namespace mmpc {
@@ -386,12 +386,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
     // first row q of Y = L^-1 [H_wx | -R] that can be nonzero in column j (the -R block is lower triangular)
     auto ylo = [](int j) constexpr { return (j < NX || !(F64 || MMPC_LANE_YLO32)) ? 0 : j - NX; };
     constexpr bool JACH = HasJacH<Model>::value && (F64 || MMPC_LANE_JACH32);
-    // FUSE_FWD (fp64 factor): the step sweep evaluates the alpha = 1 trial point with its Jacobian and forms there
+    // FUSE_FWD: the step sweep evaluates the alpha = 1 trial point with its Jacobian and forms there
     // everything pass (1) of the next iteration computes at that point (defects, d, J, |c|_1, max|c|), so when the
     // full step is accepted (99.7 % of the cfg#3 iterations, every one after the first: tools/alpha_stats.py) the
     // next iteration starts at (2).  This saves the value-only trial evaluation and pass (1)'s sweep (cfg#3:
-    // 11.63 -> 11.20 ms); the fp32-factor build (cfg#5) spills more with it (10.05 -> 11.77 ms) and keeps the
-    // separate pass.  fwd_ready: C and D of the workspace hold the accepted iterate's values.
+    // 11.63 -> 11.20 ms).  The fp32-factor build (cfg#5) spilled more with it in round 2 (10.05 -> 11.77 ms); with
+    // the directional derivative instead of the trial Jacobian (round 4) it gains there too (7.70 -> 7.34 ms,
+    // profiles/r04/ab_fwd).  fwd_ready: C and D of the workspace hold the accepted iterate's values.
     constexpr bool FUSE_FWD = FUSE_TRIAL && (std::is_same<FT, double>::value || MMPC_LANE_FWD32);
     bool fwd_ready = false;
     double J0n = 0.0, c1n = 0.0, cmaxn = 0.0;
