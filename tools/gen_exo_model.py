@@ -154,27 +154,6 @@ def main():
             coefs.append(v)
         return f"K[{cindex[v]}]"
 
-    def emit_poly(pe):
-        terms = sp.Poly(pe, *gens).terms()
-        const = 0.0
-        parts = []
-        for mon, coef in terms:
-            if all(e == 0 for e in mon):
-                const = float(coef)
-                continue
-            fac = []
-            for v, e in zip(names, mon):
-                if e == 1:
-                    fac.append(v)
-                elif e > 1:
-                    fac.append(f"{v}_{e}")
-                    used.add((v, e))
-            parts.append((float(coef), " * ".join(fac)))
-        expr = cref(const) if const != 0.0 else "0.0"
-        for coef, mono in parts:
-            expr = f"fma({cref(coef)}, {mono}, {expr})"
-        return expr, len(parts)
-
     # Horner form (round 4): the expanded monomial sums cost one product chain per monomial; nested in the variable
     # order that prints the fewest operations (sympy horner over a set of orders) the same polynomials take ~30 %
     # fewer FP64 operations.  Every nesting level is one fma(variable, inner, rest) with the coefficients from the
@@ -286,7 +265,8 @@ def main():
     for a, b in pairs:
         d2lines.append(f"    if (I == {a + 1} && J == {b + 1}) {{")
         for i, pe in enumerate(d2polys[(a, b)]):
-            e, n = emit_poly(pe)
+            e, _ = emit_horner(pe)
+            n = len(sp.Poly(pe, *gens).terms()) if pe != 0 else 0
             nd2mono += n
             d2lines.append(f"        d2M[{i}] = {e};")
         d2lines.append("    }")
