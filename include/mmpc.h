@@ -283,6 +283,20 @@ int mmpc_multi_solve_batch_host(mmpc_multi* m, int64_t B, const double* x0, cons
                                 const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
                                 int32_t* iters, double* kkt_res);
 
+/* The same solve through RCCL (SURVEY.md 8e's single-process design; replaces the per-tick m_solver call of
+ * ModelControl.cpp:159 for a batch resident on one GPU): DEVICE pointers on the multi handle's FIRST device; shard g
+ * (mmpc_shard) of every input goes to device g by ncclSend/ncclRecv, shared weights and u_lb/u_ub (device [nu] or
+ * NULL) by ncclBroadcast, every device solves its shard, and V / status / iters / kkt_res come back to the first
+ * device by ncclSend/ncclRecv (ncclCommInitAll over the listed devices at the first call).  The devices must be
+ * distinct (RCCL refuses a device listed twice: MMPC_ERR_UNSUPPORTED); RCCL is loaded with dlopen at the first call
+ * (MMPC_ERR_UNSUPPORTED when librccl is absent).  Synchronous; results equal a single-device solve bit for bit. */
+int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, const double* u_prev,
+                                const double* traj, const double* weights, int64_t weights_stride,
+                                const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
+                                int32_t* iters, double* kkt_res);
+/* the version of the RCCL library the call above loads (ncclGetVersion, e.g. 22606), MMPC_ERR_UNSUPPORTED if none */
+int mmpc_rccl_version(int32_t* version);
+
 const char* mmpc_status_string(int32_t status);
 /* thread-local description of the last API error on this thread ("" if none) */
 const char* mmpc_last_error(void);

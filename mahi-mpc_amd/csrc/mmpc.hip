@@ -19,6 +19,9 @@
 #include <type_traits>
 #include <vector>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>   // types and enums only: RCCL itself is loaded with dlopen at the first RCCL call
+
 #include "../../include/mmpc.h"
 #include "json_lite.h"
 #include "group_launch.h"
@@ -1227,10 +1230,58 @@ int mmpc_shard(int64_t B, int32_t n, int32_t i, int64_t* first, int64_t* count) 
 
 }  // extern "C"
 
+namespace {
+// RCCL entry points, resolved from librccl at the first RCCL call (no link-time dependency of libmmpc.so on it)
+struct RcclApi {
+    void* lib = nullptr;
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclBroadcast) broadcast = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclGetVersion) get_version = nullptr;
+};
+const RcclApi* rccl_api() {
+    static const RcclApi api = [] {
+        RcclApi a;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            a.lib = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (a.lib) break;
+        }
+        if (!a.lib) return a;
+        bool ok = true;
+        auto sym = [&](auto& fn, const char* n) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(a.lib, n));
+            ok &= fn != nullptr;
+        };
+        sym(a.comm_init_all, "ncclCommInitAll");
+        sym(a.comm_destroy, "ncclCommDestroy");
+        sym(a.group_start, "ncclGroupStart");
+        sym(a.group_end, "ncclGroupEnd");
+        sym(a.send, "ncclSend");
+        sym(a.recv, "ncclRecv");
+        sym(a.broadcast, "ncclBroadcast");
+        sym(a.error_string, "ncclGetErrorString");
+        sym(a.get_version, "ncclGetVersion");
+        if (!ok) a.lib = nullptr;
+        return a;
+    }();
+    return api.lib ? &api : nullptr;
+}
+}  // namespace
+
 struct mmpc_multi {
     std::vector<mmpc_handle*> h;  // one handle (own stream, workspace, staging) per listed device
     std::vector<int32_t> dev;
     std::mutex mu;                // one multi-device solve at a time
+    // RCCL path (mmpc_multi_solve_batch_rccl): one communicator and stream per device, grown-only shard buffers
+    std::vector<ncclComm_t> comm;
+    std::vector<hipStream_t> st;
+    std::vector<char*> buf;
+    std::vector<size_t> buf_bytes;
 };
 
 extern "C" {
@@ -1265,6 +1316,14 @@ int mmpc_multi_create(const char* model_json_path, const mmpc_opts* opts, const 
 
 int mmpc_multi_destroy(mmpc_multi* m) {
     if (!m) return MMPC_OK;
+    if (const RcclApi* R = rccl_api())
+        for (ncclComm_t c : m->comm)
+            if (c) R->comm_destroy(c);
+    for (size_t g = 0; g < m->st.size(); ++g) {
+        DeviceGuard dg(m->dev[g]);
+        if (m->st[g]) (void)hipStreamDestroy(m->st[g]);
+        if (m->buf[g]) (void)hipFree(m->buf[g]);
+    }
     for (mmpc_handle* h : m->h) mmpc_destroy(h);
     delete m;
     return MMPC_OK;
@@ -1321,6 +1380,161 @@ int mmpc_multi_solve_batch_host(mmpc_multi* m, int64_t B, const double* x0, cons
         if (rcs[static_cast<size_t>(g)])
             return fail(rcs[static_cast<size_t>(g)], "device " + std::to_string(m->dev[static_cast<size_t>(g)]) + ": " +
                                                          errs[static_cast<size_t>(g)]);
+    return MMPC_OK;
+}
+
+int mmpc_rccl_version(int32_t* version) {
+    if (!version) return fail(MMPC_ERR_INVALID_ARG, "null argument");
+    *version = 0;
+    const RcclApi* R = rccl_api();
+    if (!R) return fail(MMPC_ERR_UNSUPPORTED, "librccl not loadable");
+    int v = 0;
+    if (R->get_version(&v) != ncclSuccess) return fail(MMPC_ERR_UNSUPPORTED, "ncclGetVersion failed");
+    *version = v;
+    return MMPC_OK;
+}
+
+int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, const double* u_prev, const double* traj,
+                                const double* weights, int64_t weights_stride, const double* u_lb, const double* u_ub,
+                                double* V_inout, int32_t* status, int32_t* iters, double* kkt_res) {
+    if (!m) return fail(MMPC_ERR_INVALID_ARG, "null multi-device handle");
+    if (B < 0 || weights_stride < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0 or weights_stride < 0");
+    if (B == 0) return MMPC_OK;
+    if (!x0 || !u_prev || !traj || !weights || !V_inout) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
+    if ((u_lb == nullptr) != (u_ub == nullptr)) return fail(MMPC_ERR_INVALID_ARG, "u_lb and u_ub go together");
+    std::lock_guard<std::mutex> lk(m->mu);
+    const int32_t G = static_cast<int32_t>(m->h.size());
+    for (int32_t a = 0; a < G; ++a)
+        for (int32_t b = 0; b < a; ++b)
+            if (m->dev[a] == m->dev[b])
+                return fail(MMPC_ERR_UNSUPPORTED, "RCCL needs distinct devices (device " + std::to_string(m->dev[a]) +
+                                                      " listed twice); mmpc_multi_solve_batch_host shares a device");
+    const RcclApi* R = rccl_api();
+    if (!R) return fail(MMPC_ERR_UNSUPPORTED, "librccl not loadable");
+    auto nccl = [&](ncclResult_t r, const char* what) {
+        return r == ncclSuccess ? MMPC_OK : fail(MMPC_ERR_HIP, std::string(what) + ": " + R->error_string(r));
+    };
+    if (m->comm.empty()) {   // one communicator per device, in the listed order (rank g = device g of the handle)
+        std::vector<ncclComm_t> comm(static_cast<size_t>(G), nullptr);
+        std::vector<int> devs(m->dev.begin(), m->dev.end());
+        if (int rc = nccl(R->comm_init_all(comm.data(), G, devs.data()), "ncclCommInitAll")) return rc;
+        m->comm = comm;
+        m->st.assign(static_cast<size_t>(G), nullptr);
+        m->buf.assign(static_cast<size_t>(G), nullptr);
+        m->buf_bytes.assign(static_cast<size_t>(G), 0);
+        for (int32_t g = 0; g < G; ++g) {
+            DeviceGuard dg(m->dev[g]);
+            MMPC_HIP(hipStreamCreateWithFlags(&m->st[g], hipStreamNonBlocking));
+        }
+    }
+    const mmpc_model_info& mi = m->h[0]->info;
+    const int64_t nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes, NV = mi.num_v, nw = nx + 2 * nu;
+    const bool shared_w = weights_stride == 0;
+    const int64_t wst = shared_w ? 0 : weights_stride;
+    struct Shard {
+        int64_t first = 0, count = 0;
+        double *x0, *up, *tr, *w, *lb, *ub, *V, *kkt;
+        int32_t *st, *it;
+    };
+    std::vector<Shard> sh(static_cast<size_t>(G));
+    for (int32_t g = 0; g < G; ++g) {   // shard buffers on device g (grown only)
+        Shard& s = sh[static_cast<size_t>(g)];
+        mmpc_shard(B, G, g, &s.first, &s.count);
+        const int64_t c = s.count;
+        const int64_t nd = c * (nx + nu + N * nx + NV + 1) + (shared_w ? nw : c * wst) + 2 * nu;
+        const size_t bytes = static_cast<size_t>(nd) * sizeof(double) + static_cast<size_t>(2 * c) * sizeof(int32_t) + 64;
+        DeviceGuard dg(m->dev[g]);
+        if (bytes > m->buf_bytes[g]) {
+            if (m->buf[g]) MMPC_HIP(hipFree(m->buf[g]));
+            m->buf[g] = nullptr;
+            m->buf_bytes[g] = 0;
+            MMPC_HIP(hipMalloc(&m->buf[g], bytes));
+            m->buf_bytes[g] = bytes;
+        }
+        double* p = reinterpret_cast<double*>(m->buf[g]);
+        s.x0 = p; p += c * nx;
+        s.up = p; p += c * nu;
+        s.tr = p; p += c * N * nx;
+        s.V = p; p += c * NV;
+        s.kkt = p; p += c;
+        s.w = p; p += shared_w ? nw : c * wst;
+        s.lb = p; p += nu;
+        s.ub = p; p += nu;
+        s.st = reinterpret_cast<int32_t*>(p);
+        s.it = s.st + c;
+    }
+    // the caller's inputs on the first device are complete before RCCL reads them
+    {
+        DeviceGuard dg(m->dev[0]);
+        MMPC_HIP(hipDeviceSynchronize());
+    }
+    // scatter: shard g of every input from rank 0 to rank g (rank 0 included: its shard goes through RCCL as well),
+    // shared weights and the bounds by broadcast
+    const ncclDataType_t f64 = ncclFloat64, i32 = ncclInt32;
+    if (int rc = nccl(R->group_start(), "ncclGroupStart")) return rc;
+    for (int32_t g = 0; g < G; ++g) {
+        const Shard& s = sh[static_cast<size_t>(g)];
+        ncclComm_t c0 = m->comm[0], cg = m->comm[static_cast<size_t>(g)];
+        hipStream_t s0 = m->st[0], sg = m->st[static_cast<size_t>(g)];
+        if (s.count > 0) {
+            const size_t c = static_cast<size_t>(s.count);
+            R->send(x0 + s.first * nx, c * nx, f64, g, c0, s0);
+            R->recv(s.x0, c * nx, f64, 0, cg, sg);
+            R->send(u_prev + s.first * nu, c * nu, f64, g, c0, s0);
+            R->recv(s.up, c * nu, f64, 0, cg, sg);
+            R->send(traj + s.first * N * nx, c * N * nx, f64, g, c0, s0);
+            R->recv(s.tr, c * N * nx, f64, 0, cg, sg);
+            R->send(V_inout + s.first * NV, c * NV, f64, g, c0, s0);
+            R->recv(s.V, c * NV, f64, 0, cg, sg);
+            if (!shared_w) {
+                R->send(weights + s.first * wst, c * wst, f64, g, c0, s0);
+                R->recv(s.w, c * wst, f64, 0, cg, sg);
+            }
+        }
+        if (shared_w) R->broadcast(weights, s.w, static_cast<size_t>(nw), f64, 0, cg, sg);
+        if (u_lb) {
+            R->broadcast(u_lb, s.lb, static_cast<size_t>(nu), f64, 0, cg, sg);
+            R->broadcast(u_ub, s.ub, static_cast<size_t>(nu), f64, 0, cg, sg);
+        }
+    }
+    if (int rc = nccl(R->group_end(), "ncclGroupEnd (scatter)")) return rc;
+    // solve: every device its shard, on its stream after its receives
+    for (int32_t g = 0; g < G; ++g) {
+        const Shard& s = sh[static_cast<size_t>(g)];
+        if (s.count == 0) continue;
+        const int rc = mmpc_solve_batch(m->h[static_cast<size_t>(g)], s.count, s.x0, s.up, s.tr, s.w, wst,
+                                        u_lb ? s.lb : nullptr, u_lb ? s.ub : nullptr, s.V, s.st, s.it, s.kkt,
+                                        m->st[static_cast<size_t>(g)]);
+        if (rc) return fail(rc, "device " + std::to_string(m->dev[static_cast<size_t>(g)]) + ": " + g_last_error);
+    }
+    // gather: V, status, iters, kkt_res of shard g back to rank 0 at the shard's offset
+    if (int rc = nccl(R->group_start(), "ncclGroupStart")) return rc;
+    for (int32_t g = 0; g < G; ++g) {
+        const Shard& s = sh[static_cast<size_t>(g)];
+        if (s.count == 0) continue;
+        const size_t c = static_cast<size_t>(s.count);
+        ncclComm_t c0 = m->comm[0], cg = m->comm[static_cast<size_t>(g)];
+        hipStream_t s0 = m->st[0], sg = m->st[static_cast<size_t>(g)];
+        R->send(s.V, c * NV, f64, 0, cg, sg);
+        R->recv(V_inout + s.first * NV, c * NV, f64, g, c0, s0);
+        if (status) {
+            R->send(s.st, c, i32, 0, cg, sg);
+            R->recv(status + s.first, c, i32, g, c0, s0);
+        }
+        if (iters) {
+            R->send(s.it, c, i32, 0, cg, sg);
+            R->recv(iters + s.first, c, i32, g, c0, s0);
+        }
+        if (kkt_res) {
+            R->send(s.kkt, c, f64, 0, cg, sg);
+            R->recv(kkt_res + s.first, c, f64, g, c0, s0);
+        }
+    }
+    if (int rc = nccl(R->group_end(), "ncclGroupEnd (gather)")) return rc;
+    for (int32_t g = 0; g < G; ++g) {
+        DeviceGuard dg(m->dev[g]);
+        MMPC_HIP(hipStreamSynchronize(m->st[static_cast<size_t>(g)]));
+    }
     return MMPC_OK;
 }
 

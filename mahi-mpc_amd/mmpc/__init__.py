@@ -119,6 +119,8 @@ def lib(path: str | None = None):
         L.mmpc_multi_num_devices.argtypes = [_vp, C.POINTER(C.c_int32)]
         L.mmpc_multi_handle.argtypes = [_vp, C.c_int32, C.POINTER(_vp)]
         L.mmpc_multi_solve_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 6
+        L.mmpc_multi_solve_batch_rccl.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 6
+        L.mmpc_rccl_version.argtypes = [C.POINTER(C.c_int32)]
         L.mmpc_resolve_kkt_solver.argtypes = [_vp, C.c_int64, C.POINTER(C.c_int32)]
         L.mmpc_resolve_hessian.argtypes = [_vp, C.c_int64, C.c_int32, C.POINTER(C.c_int32)]
         L.mmpc_set_state_bounds.argtypes = [_vp, _vp, _vp]
@@ -428,6 +430,16 @@ class MultiSolver:
                                                    _ptr(lb), _ptr(ub), _ptr(V), _ptr(st), _ptr(it), _ptr(kkt)), self._L)
         return dict(V=V, status=st, iters=it, kkt=kkt)
 
+    def solve_batch_rccl(self, x0, u_prev, traj, weights, V, status=None, iters=None, kkt=None, u_lb=None,
+                         u_ub=None):
+        """mmpc_multi_solve_batch_rccl: torch tensors on the FIRST device of the handle (fp64, contiguous; weights
+        [nx+2nu] shared or [B][nx+2nu]); V is updated in place, status / iters (int32) / kkt filled if given."""
+        B = x0.shape[0]
+        ws = 0 if weights.dim() == 1 else weights.shape[-1]
+        p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
+        _check(self._L.mmpc_multi_solve_batch_rccl(self._m, B, p(x0), p(u_prev), p(traj), p(weights), ws, p(u_lb),
+                                                   p(u_ub), p(V), p(status), p(iters), p(kkt)), self._L)
+
     def close(self):
         if getattr(self, "_m", None):
             self._L.mmpc_multi_destroy(self._m)
@@ -438,6 +450,12 @@ class MultiSolver:
             self.close()
         except Exception:
             pass
+
+
+def rccl_version() -> int:
+    """ncclGetVersion of the RCCL the multi-device RCCL path loads (mmpc_rccl_version), e.g. 22606; 0 if none"""
+    v = C.c_int32()
+    return v.value if lib().mmpc_rccl_version(C.byref(v)) == OK else 0
 
 
 def flops_per_iteration(N: int, nx: int = 4, nu: int = 2) -> dict:

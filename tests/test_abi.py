@@ -218,3 +218,11 @@ def test_shard_partition_matches_multiprocess_split(mmpc_mod):
     for bad in ((-1, 2, 0), (10, 0, 0), (10, 2, 2), (10, 2, -1)):
         with pytest.raises(mmpc_mod.MmpcError):
             mmpc_mod.shard(*bad)
+
+
+def test_rccl_is_loadable_for_the_multi_device_path(mmpc_mod):
+    """mmpc_multi_solve_batch_rccl loads librccl with dlopen (no link-time dependency): the version it would use"""
+    v = mmpc_mod.rccl_version()
+    if not os.path.exists("/opt/rocm/lib/librccl.so.1"):
+        pytest.skip("no librccl in this image")
+    assert v >= 21000, v

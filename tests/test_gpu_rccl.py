@@ -128,3 +128,54 @@ def test_bench_rccl_flag(rccl):
     assert out["process_group"] == {"backend": "nccl", "world_size": 1, "rccl_version": rccl}
     assert out["gathered_results_match"] is True and out["converged"] == 4096
     assert out["zero_copy_results_checked"] is True
+
+
+# ---- the C-ABI's own RCCL path: one process over the listed devices (mmpc_multi_solve_batch_rccl) ----
+
+def _multi_model(mmpc_mod, tmp_path):
+    return mmpc_mod.write_model_json(str(tmp_path / "m.json"), "two_link_arm", 4, 2, 2000, 30, model="two_link_arm")
+
+
+@pytest.mark.parametrize("variant", ["shared", "bounded", "per_instance", "warm"])
+def test_multi_rccl_equals_single_device(variant, mmpc_mod, oracle, tmp_path):
+    """ncclCommInitAll over device 0, the shard sent to itself by ncclSend/ncclRecv, weights and bounds by
+    ncclBroadcast, results gathered back: bit for bit the single-handle device solve of the same instances"""
+    import torch
+    path = _multi_model(mmpc_mod, tmp_path)
+    B, N = 333, 30
+    x0, up, tr = oracle.synth(5, 0, B, N, 0.002)
+    w = np.array(WEIGHTS_CFG, dtype=np.float64)
+    if variant == "per_instance":
+        w = np.tile(w, (B, 1)) * (1.0 + 0.01 * np.arange(B))[:, None]
+    d = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device="cuda:0")
+    lb = ub = None
+    if variant == "bounded":
+        lb, ub = d(np.full(2, -2.0)), d(np.full(2, 2.0))
+    V0 = np.zeros((B, 30 * 6 + 4))
+    if variant == "warm":
+        V0 = np.ascontiguousarray(mmpc_mod.Solver(path).solve_batch_host(x0, up, tr, w)["V"] * (1.0 + 1e-3))
+    m = mmpc_mod.MultiSolver(path, [0])
+    V = d(V0)
+    st = torch.zeros(B, dtype=torch.int32, device="cuda:0")
+    it = torch.zeros_like(st)
+    kk = torch.zeros(B, dtype=torch.float64, device="cuda:0")
+    m.solve_batch_rccl(d(x0), d(up), d(tr), d(w), V, st, it, kk, u_lb=lb, u_ub=ub)
+    s = mmpc_mod.Solver(path)
+    V1 = d(V0)
+    st1, it1, kk1 = torch.zeros_like(st), torch.zeros_like(it), torch.zeros_like(kk)
+    s.solve_batch(B, d(x0), d(up), d(tr), d(w), V1, st1, it1, kk1, weights_stride=8 if w.ndim == 2 else 0,
+                  u_lb=lb, u_ub=ub)
+    torch.cuda.synchronize()
+    assert torch.equal(V, V1) and torch.equal(st, st1) and torch.equal(it, it1) and torch.equal(kk, kk1)
+    assert (st == 0).all()
+    m.close()
+
+
+def test_multi_rccl_rejects_a_repeated_device(mmpc_mod, tmp_path):
+    """RCCL refuses two ranks on one device: the RCCL entry point says so instead of hanging"""
+    import torch
+    m = mmpc_mod.MultiSolver(_multi_model(mmpc_mod, tmp_path), [0, 0])
+    t = lambda *s: torch.zeros(*s, dtype=torch.float64, device="cuda:0")
+    with pytest.raises(mmpc_mod.MmpcError):
+        m.solve_batch_rccl(t(4, 4), t(4, 2), t(4, 30, 4), t(8), t(4, 184))
+    m.close()
