@@ -35,6 +35,9 @@
 #ifndef MMPC_LANE_LB32
 #define MMPC_LANE_LB32 1
 #endif
+#ifndef MMPC_LANE_XB_BATCHED
+#define MMPC_LANE_XB_BATCHED 1
+#endif
 #ifndef MMPC_LANE_FWD32
 #define MMPC_LANE_FWD32 1
 #endif
@@ -1003,7 +1006,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                     double du[NU];
                     const gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
                     const gmem<FT>* const kk = (const gmem<FT>*)(kb + NU * 64) + lane;
-                    if constexpr (!XB) {
+                    if constexpr (!XB || MMPC_LANE_XB_BATCHED) {
                         // all loads of [K_k | kff_k] issued before the first use: under register pressure the
                         // scheduler otherwise interleaves load -> vmcnt(0) -> fma, one memory round trip per gain
                         FT kv[NU * NS];
@@ -1025,11 +1028,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
                             SK(0, SF::DU, a) = t;
                         }
                     } else {
-                        // interior-point variant: loads at their uses.  The batched-load form above, compiled for
-                        // the exo interior-point instantiation with ROCm 7.2's greedy SGPR allocator, computed wrong
-                        // steps in every lane (a register-allocation defect, not the source: the same IR is right
-                        // with -mllvm -sgpr-regalloc=basic or -vgpr-regalloc=basic); this translation
-                        // unit is built with the basic SGPR allocator (lane_launch.h), and this form stays.
+                        // loads at their uses (MMPC_LANE_XB_BATCHED=0 only).  The batched form above computed wrong
+                        // steps in the exo interior-point instantiation under ROCm 7.2's greedy SGPR allocator (a
+                        // register-allocation defect, not the source); with the basic allocator this
+                        // unit is built with it is right, and it made the exo state-bounded cfg#3-size solve
+                        // 92.4 -> 74.3 ms (round 4, profiles/r04/ab_xbb).
 #pragma unroll
                         for (int a = 0; a < NU; ++a) {
                             const int base = a * NS;
