@@ -6,13 +6,17 @@
 One "step" = one cold-started batched SQP solve of B independent instances per GPU (cfg#2: 2-link arm, nx=4,
 nu=2, N=30, h=2 ms, fp64), i.e. what the reference does per control tick in ModelControl::calc_u
 (src/Mahi/Mpc/ModelControl.cpp:116-172) -- from V = 0 with x_0 pinned, the reference's first-call state -- for
-B instances at once, THROUGH RESULTS ON HOST: every step ends with the per-instance results the
+B instances at once, FROM INPUT STAGING THROUGH RESULTS ON HOST: every step first generates its B
+instances on the device (mmpc_synth_batch from (seed, global instance index), the per-tick packing of
+ModelControl.cpp:118-157) and ends with the per-instance results the
 reference consumes (u_0*, status, iterations; ModelControl.cpp:160-190) in pinned host memory -- stored there
 by the solve kernel itself (mmpc_solve_batch_u0 into mmpc_host_alloc memory, each rank into its own process's
 host memory); with N > 1 the last step's results of all ranks are also gathered to rank 0 (RCCL
-all_gather_into_tensor, then D2H) and checked there.  Inputs are generated on the device from
-(seed, global instance index) before the timed region (weak scaling: rank r solves global instances
-[r B, (r+1) B); results do not depend on the GPU count).
+all_gather_into_tensor, then D2H) and checked there.  Step k of the timed region solves the instance block
+max(K - 2 - k, 0) (global instances block * B_total + [r B, (r+1) B) on rank r, weak scaling): the steps solve
+distinct instances, and the last two the block 0 that the CPU baseline and the N > 1 zero-copy check compare
+against; results do not depend on the GPU count.  `value_solve_only` beside `value` is a second timed loop of the
+same K solves on resident inputs (no generation): its HIP-event bracket is also the kernel time of the roofline.
 
 Multi-GPU: ``--gpus N`` with N > 1 and no WORLD_SIZE in the environment makes this process a launcher that
 starts N rank processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each) before anything touches
@@ -402,13 +406,18 @@ def run_config(args, name, world, rank, primary=True):
         else:
             solver.solve_batch(n, x0, up, tr, w, V, st, it, None, stream=sh, u_lb=ulb, u_ub=uub)
 
-    def solve(k, last):
+    def block(k):   # instance block of timed step k; warm-up step j generates block K + j (never timed)
+        return max(args.steps - 2 - k, 0)
+
+    def solve(k, last, blk=None):
+        if blk is not None:   # this step's instances, generated on the device inside the clock
+            solver.synth(SEED, blk * Bt + first, n, x0, up, tr, stream=sh)
         if zero_v:
             V.zero_()   # cold start (reference first call: v_init = 0, ModelControl.cpp:29-50)
         launch(k, last)
 
     for k in range(args.warmup):   # the last warm-up step also initialises the RCCL gather (N > 1)
-        solve(k, args.warmup - 1)
+        solve(k, args.warmup - 1, args.steps + k)
         results_to_host(k, args.warmup - 1)
     sync = (lambda: torch.cuda.synchronize(dev)) if not standin else (lambda: None)
     sync()
@@ -425,7 +434,7 @@ def run_config(args, name, world, rank, primary=True):
     if ev:
         ev[0].record(stream)
     for k in range(args.steps):
-        solve(k, args.steps - 1)
+        solve(k, args.steps - 1, block(k))
         if ev and k == args.steps - 1:
             ev[1].record(stream)   # after the last launch (N > 1: before its result gather)
         results_to_host(k, args.steps - 1)
@@ -433,8 +442,26 @@ def run_config(args, name, world, rank, primary=True):
     if coll:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = ev[0].elapsed_time(ev[1]) / args.steps if ev else 0.0
+    step_ms = ev[0].elapsed_time(ev[1]) / args.steps if ev else 0.0   # generation + solve, per step
     elapsed = mdist.max_over_ranks(elapsed, device=dev)
+    # the same K solves again on the resident inputs of the last step (block 0), without the generation: the
+    # solve-only rate beside the line's value, and the solve kernel's own mean duration for the roofline
+    if coll:
+        dist.barrier()
+    sync()
+    t1 = time.perf_counter()
+    if ev:
+        ev[0].record(stream)
+    for k in range(args.steps):
+        solve(k, args.steps - 1)
+        if ev and k == args.steps - 1:
+            ev[1].record(stream)
+        results_to_host(k, args.steps - 1)
+    sync()
+    if coll:
+        dist.barrier()
+    elapsed_solve = mdist.max_over_ranks(time.perf_counter() - t1, device=dev)
+    kern_ms = ev[0].elapsed_time(ev[1]) / args.steps if ev else 0.0
 
     def hbytes(k):
         return torch.from_numpy(np.frombuffer(hbuf[k % 2]._buf, dtype=np.uint8).copy())
@@ -475,6 +502,8 @@ def run_config(args, name, world, rank, primary=True):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "value_solve_only": total / elapsed_solve,
+        "ms_per_step_solve_only": elapsed_solve / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
@@ -498,8 +527,11 @@ def run_config(args, name, world, rank, primary=True):
                                    "step's table gathered to rank 0 by RCCL all_gather_into_tensor + D2H"
                                    if coll else "batch-shard x1; per-step results (u_0*, status, iters) stored "
                                                      "by the solve kernel into pinned host memory (mmpc_host_alloc)"),
-                   "timed_region": ("cold-start solves + per-step results (u_0*, status, iters) on the host"
-                                    + ("; the last step's table of all ranks on rank 0's host" if coll else ""))},
+                   "timed_region": ("per step: on-device generation of the step's instances (mmpc_synth_batch, "
+                                    "the per-tick input packing) + cold-start solve + results (u_0*, status, iters) "
+                                    "on the host"
+                                    + ("; the last step's table of all ranks on rank 0's host" if coll else "")
+                                    + "; value_solve_only: the same K solves on resident inputs")},
         "converged": conv,
         "gathered_results_match": ok,
         "zero_copy_results_checked": zc_ok is not None,
@@ -516,6 +548,7 @@ def run_config(args, name, world, rank, primary=True):
                                            .view(Bc, nu)[:nrows[r], 0].tolist()]
     else:
         out["kernel_ms"] = kern_ms
+        out["step_gpu_ms"] = step_ms   # generation + solve kernels of one step (HIP events)
         out["roofline"] = roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, n, iters, kern_ms, hess)
     if name == "cfg5" and world == 1 and not standin and not args.no_sweep:
         out["tolerance_sweep"] = cfg5_sweep(path, cfg, n, x0, up, tr, w, args.hessian)

@@ -289,11 +289,15 @@ int mmpc_multi_solve_batch_host(mmpc_multi* m, int64_t B, const double* x0, cons
  * NULL) by ncclBroadcast, every device solves its shard, and V / status / iters / kkt_res come back to the first
  * device by ncclSend/ncclRecv (ncclCommInitAll over the listed devices at the first call).  The devices must be
  * distinct (RCCL refuses a device listed twice: MMPC_ERR_UNSUPPORTED); RCCL is loaded with dlopen at the first call
- * (MMPC_ERR_UNSUPPORTED when librccl is absent).  Synchronous; results equal a single-device solve bit for bit. */
+ * (MMPC_ERR_UNSUPPORTED when librccl is absent).  `stream` (hipStream_t on the first device, NULL = the null
+ * stream): the call's first RCCL operation is ordered after the work already queued there, and work queued there
+ * later sees the results.  Per-instance weights (weights_stride >= nx + 2 nu) need (B - 1) weights_stride + nx + 2 nu
+ * doubles.  Every RCCL operation's result is checked; after an error every stream of the call is drained before the
+ * call returns.  Synchronous; results equal a single-device solve bit for bit. */
 int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, const double* u_prev,
                                 const double* traj, const double* weights, int64_t weights_stride,
                                 const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
-                                int32_t* iters, double* kkt_res);
+                                int32_t* iters, double* kkt_res, void* stream);
 /* the version of the RCCL library the call above loads (ncclGetVersion, e.g. 22606), MMPC_ERR_UNSUPPORTED if none */
 int mmpc_rccl_version(int32_t* version);
 

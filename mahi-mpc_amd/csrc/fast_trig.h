@@ -10,8 +10,10 @@
 // argument: ~40 VALU instructions with the 16 constants read as scalar loads (s_load) from a constant table.
 //
 // Accuracy: |x| <= 2^20 pi/2: within 1 ulp of libm (absolute error <= 1.2e-16) in tests/test_fast_trig.py (random
-// arguments up to 1.6e6 and the multiples of pi/2 up to 1e5 pi/2).  Beyond that the reduction
-// loses bits (absolute error grows like |x| 2^-104); NaN and +-inf give NaN, as the device library.
+// arguments up to 1.6e6 and the multiples of pi/2 up to 1e5 pi/2).  Beyond that the reduction would lose bits: the
+// device build returns NaN there (only a diverging iterate gets that far; the solver then reports the instance
+// non-finite), the host build switches to libm.  The quadrant is formed without an out-of-range int conversion for
+// every x.  NaN and +-inf give NaN, as the device library.
 #pragma once
 #include <math.h>
 
@@ -52,10 +54,20 @@ inline trig_cptr trig_table() { return kTrigConst; }
 
 // s = sin x, c = cos x; K = trig_table() (one table pointer may serve several calls of one evaluation)
 MMPC_TRIG_FN void sincos_fast(trig_cptr K, double x, double* s, double* c) {
+#if !defined(__HIPCC__) && !defined(MMPC_TRIG_DEVICE_PATH_ON_HOST)
+    if (fabs(x) > 1647099.3291652855) {   // 2^20 pi/2: beyond it the host build (checks, oracle helpers) uses libm
+        *s = sin(x);
+        *c = cos(x);
+        return;
+    }
+#endif
     const double n = rint(x * K[0]);
     double r = fma(-n, K[1], x);
     r = fma(-n, K[2], r);
     r = fma(-n, K[3], r);
+    // beyond 2^20 pi/2 the reduction loses bits: the result is made NaN (one compare and select, no branch), so the
+    // solver reports such an iterate non-finite instead of continuing with inaccurate trig values
+    r = fabs(x) <= 1647099.3291652855 ? r : __builtin_nan("");
     const double z = r * r;
     // __kernel_sin(r, 0): r + r^3 (S1 + z (S2 + ... + z S6))
     const double ps = fma(z, fma(z, fma(z, fma(z, K[9], K[8]), K[7]), K[6]), K[5]);
@@ -65,8 +77,10 @@ MMPC_TRIG_FN void sincos_fast(trig_cptr K, double x, double* s, double* c) {
     const double hz = 0.5 * z;
     const double w = 1.0 - hz;
     const double cr = w + (((1.0 - w) - hz) + z * pc);
-    // quadrant n mod 4: sin = (sr, cr, -sr, -cr), cos = (cr, -sr, -cr, sr)
-    const int q = (int)n;
+    // quadrant n mod 4: sin = (sr, cr, -sr, -cr), cos = (cr, -sr, -cr, sr).  n mod 4 is formed in double (every step
+    // exact for |n| < 2^53), so the int conversion sees 0..3 for any finite x: no out-of-range conversion (undefined
+    // behaviour on the host, saturation on the device) however large a diverging iterate gets
+    const int q = (int)fma(-4.0, floor(0.25 * n), n);
     const bool odd = (q & 1) != 0;
     const double a = odd ? cr : sr, b = odd ? sr : cr;
     *s = (q & 2) ? -a : a;

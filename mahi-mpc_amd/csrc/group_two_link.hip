@@ -1,9 +1,11 @@
-// group_two_link.hip -- the built-in 2-link arm's 16-lane group kernels (sqp_group.h; the cfg#2 headline path) in a
-// translation unit of their own, compiled with LLVM's default (greedy) register allocators.  Every other kernel of the
-// library is built with -mllvm -sgpr-regalloc=basic (Makefile REGALLOC): ROCm 7.2's greedy SGPR allocator
-// miscompiled kernels at the 512-register limit -- five lane-kernel builds and, in round 4, the exo
-// group kernel with the exact Hessian (an illegal memory access after the exo polynomials changed form).  The 2-link
-// group kernels do not spill VGPRs and run ~1 % faster with the greedy allocator.
+// group_two_link.hip -- the built-in 2-link arm's 16-lane group kernels (sqp_group.h; the cfg#2 headline path) in
+// translation units of their own.  This file is compiled twice (Makefile):
+//   * build/group_two_link.o: the UNBOUNDED kernels (Gauss-Newton and exact Hessian, the cfg#2 path) with LLVM's
+//     default (greedy) register allocators -- they allocate without VGPR spills or scratch (tests/test_build_flags.py
+//     checks the built code object's metadata), and run ~1 % faster than with the basic SGPR allocator;
+//   * build/group_two_link_bounded.o (-DMMPC_GROUP_BOUNDED_UNIT): the control-bounded and state-bounded kernels with
+//     -mllvm -sgpr-regalloc=basic like every other unit: they reach the 512-register limit with VGPR spills to
+//     scratch, the profile of the greedy-allocator miscompiles of DESIGN.md 4b.
 #include <hip/hip_runtime.h>
 
 #include "../../include/mmpc.h"
@@ -24,18 +26,8 @@ hipError_t launch(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const S
     k<<<grid, block, lds, stream>>>(p, gwk);
     return hipGetLastError();
 }
-}  // namespace
-
-hipError_t launch_group_two_link(bool bounded, bool xb, bool exact, dim3 grid, dim3 block, size_t lds,
-                                 hipStream_t stream, const SolveParams& p, const GroupWork& gwk) {
-    if (exact) return bounded ? launch<true, false, true>(grid, block, lds, stream, p, gwk)
-                              : launch<false, false, true>(grid, block, lds, stream, p, gwk);
-    if (xb) return launch<false, true>(grid, block, lds, stream, p, gwk);
-    return bounded ? launch<true>(grid, block, lds, stream, p, gwk) : launch<false>(grid, block, lds, stream, p, gwk);
-}
-
 // this translation unit's copy of the phase-timing table (as lane_kernels.hip)
-hipError_t group_two_link_phase_cycles(unsigned long long* out16, bool reset) {
+hipError_t unit_phase_cycles(unsigned long long* out16, bool reset) {
     hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mmpc_phase_cycles), 16 * sizeof(unsigned long long));
     if (e == hipSuccess && reset) {
         unsigned long long z[16] = {0};
@@ -43,4 +35,24 @@ hipError_t group_two_link_phase_cycles(unsigned long long* out16, bool reset) {
     }
     return e;
 }
+}  // namespace
+
+#ifndef MMPC_GROUP_BOUNDED_UNIT
+hipError_t launch_group_two_link(bool exact, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
+                                 const SolveParams& p, const GroupWork& gwk) {
+    return exact ? launch<false, false, true>(grid, block, lds, stream, p, gwk)
+                 : launch<false>(grid, block, lds, stream, p, gwk);
+}
+hipError_t group_two_link_phase_cycles(unsigned long long* out16, bool reset) { return unit_phase_cycles(out16, reset); }
+#else
+hipError_t launch_group_two_link_bounded(bool xb, bool exact, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
+                                         const SolveParams& p, const GroupWork& gwk) {
+    if (xb) return launch<false, true>(grid, block, lds, stream, p, gwk);   // the interior point: Gauss-Newton only
+    return exact ? launch<true, false, true>(grid, block, lds, stream, p, gwk)
+                 : launch<true>(grid, block, lds, stream, p, gwk);
+}
+hipError_t group_two_link_bounded_phase_cycles(unsigned long long* out16, bool reset) {
+    return unit_phase_cycles(out16, reset);
+}
+#endif
 }  // namespace mmpc

@@ -758,9 +758,11 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         if (hess < 0) return hess;
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
-            if constexpr (std::is_same<M, TwoLinkArm>::value) {   // greedy-allocator unit (group_launch.h)
-                const hipError_t e = launch_group_two_link(bounded, xb, hess == MMPC_HESSIAN_EXACT, grid, block, lds,
-                                                           stream, p, gwk);
+            if constexpr (std::is_same<M, TwoLinkArm>::value) {   // the units of group_launch.h
+                const bool exact = hess == MMPC_HESSIAN_EXACT;
+                const hipError_t e =
+                    (bounded || xb) ? launch_group_two_link_bounded(xb, exact, grid, block, lds, stream, p, gwk)
+                                    : launch_group_two_link(exact, grid, block, lds, stream, p, gwk);
                 return e == hipSuccess ? MMPC_OK : fail(MMPC_ERR_HIP, std::string("group kernel launch: ") +
                                                                           hipGetErrorString(e));
             } else {
@@ -1396,13 +1398,19 @@ int mmpc_rccl_version(int32_t* version) {
 
 int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, const double* u_prev, const double* traj,
                                 const double* weights, int64_t weights_stride, const double* u_lb, const double* u_ub,
-                                double* V_inout, int32_t* status, int32_t* iters, double* kkt_res) {
+                                double* V_inout, int32_t* status, int32_t* iters, double* kkt_res, void* stream) {
     if (!m) return fail(MMPC_ERR_INVALID_ARG, "null multi-device handle");
     if (B < 0 || weights_stride < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0 or weights_stride < 0");
     if (B == 0) return MMPC_OK;
     if (!x0 || !u_prev || !traj || !weights || !V_inout) return fail(MMPC_ERR_INVALID_ARG, "null input pointer");
     if ((u_lb == nullptr) != (u_ub == nullptr)) return fail(MMPC_ERR_INVALID_ARG, "u_lb and u_ub go together");
     std::lock_guard<std::mutex> lk(m->mu);
+    const mmpc_model_info& mi = m->h[0]->info;
+    const int64_t nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes, NV = mi.num_v, nw = nx + 2 * nu;
+    // checked before anything is sent: the scatter reads rows of weights_stride (mmpc_solve_batch checks it too, but
+    // only after the shards have been sent)
+    if (weights_stride != 0 && weights_stride < nw)
+        return fail(MMPC_ERR_INVALID_ARG, "weights_stride must be 0 (shared) or >= nx + 2 nu");
     const int32_t G = static_cast<int32_t>(m->h.size());
     for (int32_t a = 0; a < G; ++a)
         for (int32_t b = 0; b < a; ++b)
@@ -1427,8 +1435,6 @@ int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, cons
             MMPC_HIP(hipStreamCreateWithFlags(&m->st[g], hipStreamNonBlocking));
         }
     }
-    const mmpc_model_info& mi = m->h[0]->info;
-    const int64_t nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes, NV = mi.num_v, nw = nx + 2 * nu;
     const bool shared_w = weights_stride == 0;
     const int64_t wst = shared_w ? 0 : weights_stride;
     struct Shard {
@@ -1463,41 +1469,67 @@ int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, cons
         s.st = reinterpret_cast<int32_t*>(p);
         s.it = s.st + c;
     }
-    // the caller's inputs on the first device are complete before RCCL reads them
+    // the caller's inputs on the first device are complete before RCCL reads them: the first device's stream waits
+    // for the caller's stream (no device-wide synchronisation); at the end the caller's stream waits for the results
+    hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
     {
         DeviceGuard dg(m->dev[0]);
-        MMPC_HIP(hipDeviceSynchronize());
+        hipEvent_t ev;
+        MMPC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(ev, caller);
+        if (e == hipSuccess) e = hipStreamWaitEvent(m->st[0], ev, 0);
+        (void)hipEventDestroy(ev);
+        MMPC_HIP(e);
     }
+    // every stream of the call drained before an error after the first enqueue is returned (no RCCL operation or
+    // solve of this call is still running when the caller sees the error)
+    auto drain = [&](int rc) {
+        for (int32_t g = 0; g < G; ++g) {
+            DeviceGuard dg(m->dev[g]);
+            (void)hipStreamSynchronize(m->st[static_cast<size_t>(g)]);
+        }
+        return rc;
+    };
+    // a group is always closed (ncclGroupEnd) even when an operation inside it failed; the first failure is reported
+    int grp_rc = MMPC_OK;
+    auto op = [&](ncclResult_t r, const char* what, int32_t g) {
+        if (r != ncclSuccess && grp_rc == MMPC_OK)
+            grp_rc = fail(MMPC_ERR_HIP, std::string(what) + " (shard " + std::to_string(g) + "): " + R->error_string(r));
+    };
     // scatter: shard g of every input from rank 0 to rank g (rank 0 included: its shard goes through RCCL as well),
-    // shared weights and the bounds by broadcast
+    // shared weights and the bounds by broadcast.  Per-instance weights: the last row of a shard is sent up to its
+    // nx + 2 nu entries, so a caller's buffer of (B - 1) weights_stride + nx + 2 nu doubles is never over-read.
     const ncclDataType_t f64 = ncclFloat64, i32 = ncclInt32;
-    if (int rc = nccl(R->group_start(), "ncclGroupStart")) return rc;
+    if (int rc = nccl(R->group_start(), "ncclGroupStart")) return drain(rc);
     for (int32_t g = 0; g < G; ++g) {
         const Shard& s = sh[static_cast<size_t>(g)];
         ncclComm_t c0 = m->comm[0], cg = m->comm[static_cast<size_t>(g)];
         hipStream_t s0 = m->st[0], sg = m->st[static_cast<size_t>(g)];
         if (s.count > 0) {
             const size_t c = static_cast<size_t>(s.count);
-            R->send(x0 + s.first * nx, c * nx, f64, g, c0, s0);
-            R->recv(s.x0, c * nx, f64, 0, cg, sg);
-            R->send(u_prev + s.first * nu, c * nu, f64, g, c0, s0);
-            R->recv(s.up, c * nu, f64, 0, cg, sg);
-            R->send(traj + s.first * N * nx, c * N * nx, f64, g, c0, s0);
-            R->recv(s.tr, c * N * nx, f64, 0, cg, sg);
-            R->send(V_inout + s.first * NV, c * NV, f64, g, c0, s0);
-            R->recv(s.V, c * NV, f64, 0, cg, sg);
+            op(R->send(x0 + s.first * nx, c * nx, f64, g, c0, s0), "ncclSend x0", g);
+            op(R->recv(s.x0, c * nx, f64, 0, cg, sg), "ncclRecv x0", g);
+            op(R->send(u_prev + s.first * nu, c * nu, f64, g, c0, s0), "ncclSend u_prev", g);
+            op(R->recv(s.up, c * nu, f64, 0, cg, sg), "ncclRecv u_prev", g);
+            op(R->send(traj + s.first * N * nx, c * N * nx, f64, g, c0, s0), "ncclSend traj", g);
+            op(R->recv(s.tr, c * N * nx, f64, 0, cg, sg), "ncclRecv traj", g);
+            op(R->send(V_inout + s.first * NV, c * NV, f64, g, c0, s0), "ncclSend V", g);
+            op(R->recv(s.V, c * NV, f64, 0, cg, sg), "ncclRecv V", g);
             if (!shared_w) {
-                R->send(weights + s.first * wst, c * wst, f64, g, c0, s0);
-                R->recv(s.w, c * wst, f64, 0, cg, sg);
+                const size_t nwc = (c - 1) * static_cast<size_t>(wst) + static_cast<size_t>(nw);
+                op(R->send(weights + s.first * wst, nwc, f64, g, c0, s0), "ncclSend weights", g);
+                op(R->recv(s.w, nwc, f64, 0, cg, sg), "ncclRecv weights", g);
             }
         }
-        if (shared_w) R->broadcast(weights, s.w, static_cast<size_t>(nw), f64, 0, cg, sg);
+        // collectives run on every rank, shards of count 0 included (the broadcast lands in its unused buffer)
+        if (shared_w) op(R->broadcast(weights, s.w, static_cast<size_t>(nw), f64, 0, cg, sg), "ncclBroadcast weights", g);
         if (u_lb) {
-            R->broadcast(u_lb, s.lb, static_cast<size_t>(nu), f64, 0, cg, sg);
-            R->broadcast(u_ub, s.ub, static_cast<size_t>(nu), f64, 0, cg, sg);
+            op(R->broadcast(u_lb, s.lb, static_cast<size_t>(nu), f64, 0, cg, sg), "ncclBroadcast u_lb", g);
+            op(R->broadcast(u_ub, s.ub, static_cast<size_t>(nu), f64, 0, cg, sg), "ncclBroadcast u_ub", g);
         }
     }
-    if (int rc = nccl(R->group_end(), "ncclGroupEnd (scatter)")) return rc;
+    if (int rc = nccl(R->group_end(), "ncclGroupEnd (scatter)")) return drain(rc);
+    if (grp_rc) return drain(grp_rc);
     // solve: every device its shard, on its stream after its receives
     for (int32_t g = 0; g < G; ++g) {
         const Shard& s = sh[static_cast<size_t>(g)];
@@ -1505,32 +1537,45 @@ int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, cons
         const int rc = mmpc_solve_batch(m->h[static_cast<size_t>(g)], s.count, s.x0, s.up, s.tr, s.w, wst,
                                         u_lb ? s.lb : nullptr, u_lb ? s.ub : nullptr, s.V, s.st, s.it, s.kkt,
                                         m->st[static_cast<size_t>(g)]);
-        if (rc) return fail(rc, "device " + std::to_string(m->dev[static_cast<size_t>(g)]) + ": " + g_last_error);
+        if (rc) {
+            const std::string err = "device " + std::to_string(m->dev[static_cast<size_t>(g)]) + ": " + g_last_error;
+            return drain(fail(rc, err));
+        }
     }
     // gather: V, status, iters, kkt_res of shard g back to rank 0 at the shard's offset
-    if (int rc = nccl(R->group_start(), "ncclGroupStart")) return rc;
+    if (int rc = nccl(R->group_start(), "ncclGroupStart")) return drain(rc);
     for (int32_t g = 0; g < G; ++g) {
         const Shard& s = sh[static_cast<size_t>(g)];
         if (s.count == 0) continue;
         const size_t c = static_cast<size_t>(s.count);
         ncclComm_t c0 = m->comm[0], cg = m->comm[static_cast<size_t>(g)];
         hipStream_t s0 = m->st[0], sg = m->st[static_cast<size_t>(g)];
-        R->send(s.V, c * NV, f64, 0, cg, sg);
-        R->recv(V_inout + s.first * NV, c * NV, f64, g, c0, s0);
+        op(R->send(s.V, c * NV, f64, 0, cg, sg), "ncclSend V (gather)", g);
+        op(R->recv(V_inout + s.first * NV, c * NV, f64, g, c0, s0), "ncclRecv V (gather)", g);
         if (status) {
-            R->send(s.st, c, i32, 0, cg, sg);
-            R->recv(status + s.first, c, i32, g, c0, s0);
+            op(R->send(s.st, c, i32, 0, cg, sg), "ncclSend status", g);
+            op(R->recv(status + s.first, c, i32, g, c0, s0), "ncclRecv status", g);
         }
         if (iters) {
-            R->send(s.it, c, i32, 0, cg, sg);
-            R->recv(iters + s.first, c, i32, g, c0, s0);
+            op(R->send(s.it, c, i32, 0, cg, sg), "ncclSend iters", g);
+            op(R->recv(iters + s.first, c, i32, g, c0, s0), "ncclRecv iters", g);
         }
         if (kkt_res) {
-            R->send(s.kkt, c, f64, 0, cg, sg);
-            R->recv(kkt_res + s.first, c, f64, g, c0, s0);
+            op(R->send(s.kkt, c, f64, 0, cg, sg), "ncclSend kkt", g);
+            op(R->recv(kkt_res + s.first, c, f64, g, c0, s0), "ncclRecv kkt", g);
         }
     }
-    if (int rc = nccl(R->group_end(), "ncclGroupEnd (gather)")) return rc;
+    if (int rc = nccl(R->group_end(), "ncclGroupEnd (gather)")) return drain(rc);
+    if (grp_rc) return drain(grp_rc);
+    {   // later work on the caller's stream sees the gathered results
+        DeviceGuard dg(m->dev[0]);
+        hipEvent_t ev;
+        MMPC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        hipError_t e = hipEventRecord(ev, m->st[0]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(caller, ev, 0);
+        (void)hipEventDestroy(ev);
+        if (e != hipSuccess) return drain(fail(MMPC_ERR_HIP, std::string("event: ") + hipGetErrorString(e)));
+    }
     for (int32_t g = 0; g < G; ++g) {
         DeviceGuard dg(m->dev[g]);
         MMPC_HIP(hipStreamSynchronize(m->st[static_cast<size_t>(g)]));
@@ -1565,7 +1610,9 @@ int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) {
     MMPC_HIP(lane_phase_cycles(lane, reset != 0));
     for (int i = 0; i < 16; ++i) out16[i] += lane[i];
 #if MMPC_BUILTIN_MODELS
-    MMPC_HIP(group_two_link_phase_cycles(lane, reset != 0));   // the 2-link group kernels' unit (group_launch.h)
+    MMPC_HIP(group_two_link_phase_cycles(lane, reset != 0));   // the 2-link group kernels' units (group_launch.h)
+    for (int i = 0; i < 16; ++i) out16[i] += lane[i];
+    MMPC_HIP(group_two_link_bounded_phase_cycles(lane, reset != 0));
     for (int i = 0; i < 16; ++i) out16[i] += lane[i];
 #endif
     return MMPC_OK;

@@ -154,7 +154,12 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     const int gbase = gi * G;  // first lane of this instance's group
     const int64_t inst = (int64_t)blockIdx.x * kGroupsPerWave + gi;
     const bool valid = inst < p.B;
-    const int64_t ii = valid ? inst : 0;  // invalid groups are masked by `done` and touch instance 0 read-only
+    // a group past the end of the batch (the last wave of a B not divisible by 4) leaves at once: no group reads
+    // another group's lanes (row_bcast and the group reductions stay inside the 16-lane row) or LDS block, so
+    // nothing else in the wave needs it, and it issues no memory access at all (round 4 had those groups run on
+    // aliased to instance 0 and masked by `done`, which made every store's masking a correctness condition)
+    if (!valid) return;
+    const int64_t ii = inst;
     const int N = p.N;
     const int NV = NX * (N + 1) + NU * N;
     const double h = p.h;

@@ -119,7 +119,7 @@ def lib(path: str | None = None):
         L.mmpc_multi_num_devices.argtypes = [_vp, C.POINTER(C.c_int32)]
         L.mmpc_multi_handle.argtypes = [_vp, C.c_int32, C.POINTER(_vp)]
         L.mmpc_multi_solve_batch_host.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 6
-        L.mmpc_multi_solve_batch_rccl.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 6
+        L.mmpc_multi_solve_batch_rccl.argtypes = [_vp, C.c_int64] + [_vp] * 4 + [C.c_int64] + [_vp] * 7
         L.mmpc_rccl_version.argtypes = [C.POINTER(C.c_int32)]
         L.mmpc_resolve_kkt_solver.argtypes = [_vp, C.c_int64, C.POINTER(C.c_int32)]
         L.mmpc_resolve_hessian.argtypes = [_vp, C.c_int64, C.c_int32, C.POINTER(C.c_int32)]
@@ -431,14 +431,20 @@ class MultiSolver:
         return dict(V=V, status=st, iters=it, kkt=kkt)
 
     def solve_batch_rccl(self, x0, u_prev, traj, weights, V, status=None, iters=None, kkt=None, u_lb=None,
-                         u_ub=None):
+                         u_ub=None, weights_stride=None, stream=None):
         """mmpc_multi_solve_batch_rccl: torch tensors on the FIRST device of the handle (fp64, contiguous; weights
-        [nx+2nu] shared or [B][nx+2nu]); V is updated in place, status / iters (int32) / kkt filled if given."""
+        [nx+2nu] shared or [B][nx+2nu], or a flat buffer with an explicit weights_stride); V is updated in place,
+        status / iters (int32) / kkt filled if given.  stream: the hipStream_t (int) the inputs were produced on --
+        default torch's current stream of x0's device."""
         B = x0.shape[0]
-        ws = 0 if weights.dim() == 1 else weights.shape[-1]
+        ws = (0 if weights.dim() == 1 else weights.shape[-1]) if weights_stride is None else int(weights_stride)
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(x0.device).cuda_stream
         p = lambda t: None if t is None else C.c_void_p(t.data_ptr())
         _check(self._L.mmpc_multi_solve_batch_rccl(self._m, B, p(x0), p(u_prev), p(traj), p(weights), ws, p(u_lb),
-                                                   p(u_ub), p(V), p(status), p(iters), p(kkt)), self._L)
+                                                   p(u_ub), p(V), p(status), p(iters), p(kkt),
+                                                   C.c_void_p(stream) if stream else None), self._L)
 
     def close(self):
         if getattr(self, "_m", None):

@@ -1,8 +1,9 @@
 """CPU: the register-allocator policy of the build.  ROCm 7.2's greedy SGPR allocator miscompiled six
 kernels at the 512-register limit (five exo lane-kernel builds, the exo group kernel with the exact Hessian); every
-kernel unit is therefore compiled with -mllvm -sgpr-regalloc=basic except csrc/group_two_link.hip (the built-in 2-link
-group kernels of cfg#2, which do not spill VGPRs).  These checks keep a later edit of the Makefile or of
-ModelGenerator::compile_model from dropping the flag silently."""
+kernel unit is therefore compiled with -mllvm -sgpr-regalloc=basic except build/group_two_link.o (the built-in 2-link
+UNBOUNDED group kernels of cfg#2).  These checks keep a later edit of the Makefile or of ModelGenerator::compile_model
+from dropping the flag silently, and read the greedy unit's code object to check that none of its kernels spills VGPRs
+or uses scratch."""
 import os
 import re
 
@@ -32,8 +33,8 @@ def test_makefile_units_and_allocator():
         assert any("$(LANEFLAGS)" in l for l in r[obj]), obj
     for obj in ("build/group_two_link.o", "build/group_two_link_timing.o"):
         assert r[obj] and not any("LANEFLAGS" in l for l in r[obj]), obj
-    link = " ".join(r["lib/libmmpc.so"])
-    for obj in ("build/mmpc.o", "build/lane_kernels.o", "build/group_two_link.o"):
+    link = " ".join(r["lib/libmmpc.so"]).replace("$(OBJS)", re.search(r"^OBJS := (.*)$", text, re.M).group(1))
+    for obj in ("build/mmpc.o", "build/lane_kernels.o", "build/group_two_link.o", "build/group_two_link_bounded.o"):
         assert obj in link
 
 
@@ -53,3 +54,66 @@ def test_generated_model_libraries_use_the_basic_allocator():
     block = src[i:src.index("};", i)]
     compiles = [l for l in block.splitlines() if "-c '" in l]
     assert len(compiles) == 2 and all("-sgpr-regalloc=basic" in l for l in compiles), compiles
+
+
+# ---- the greedy unit's kernels: no VGPR spills, no scratch ----
+LLVM = "/opt/rocm/lib/llvm/bin"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+
+
+def _kernel_metadata(obj):
+    """{kernel name: {vgpr_spill_count, sgpr_spill_count, private_segment_fixed_size}} of the gfx950 code object
+    embedded in a hipcc -c object file (its .hip_fatbin offload bundle), read from the code object's metadata note"""
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "k.co")
+        subprocess.run([f"{LLVM}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", obj, os.path.join(d, "x.o")],
+                       check=True, capture_output=True)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
+                        f"--targets={TARGET}", f"--output={co}"], check=True, capture_output=True)
+        notes = subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                               text=True).stdout
+    out, cur = {}, None
+    for line in notes.splitlines():
+        m = re.match(r"\s*(?:- )?\.(name|vgpr_spill_count|sgpr_spill_count|private_segment_fixed_size):\s+(\S+)", line)
+        if not m:
+            continue
+        k, v = m.groups()
+        if k == "name":
+            if v.endswith(".kd"):
+                continue
+            cur = out.setdefault(v, {})
+        elif cur is not None:
+            cur[k] = int(v)
+    return out
+
+
+def _need(obj):
+    import pytest
+    if not os.path.exists(obj) or not os.path.exists(f"{LLVM}/clang-offload-bundler"):
+        pytest.skip(f"{obj} not built (make -C mahi-mpc_amd)")
+
+
+def test_greedy_unit_kernels_do_not_spill():
+    """Every kernel compiled with the greedy allocators allocates without VGPR spills and without scratch: the six
+    greedy miscompiles of rounds 3-4 all sat at the 512-register limit with VGPR and SGPR spills"""
+    obj = os.path.join(AMD, "build", "group_two_link.o")
+    _need(obj)
+    md = _kernel_metadata(obj)
+    kernels = {k: v for k, v in md.items() if "sqp_group_kernel" in k}
+    assert kernels, md
+    for name, v in kernels.items():
+        assert v.get("vgpr_spill_count") == 0 and v.get("private_segment_fixed_size") == 0, (name, v)
+    # only the unbounded instantiations <TwoLinkArm, BOUNDED = false, XB = false, EXACT> live in the greedy unit
+    assert all("TwoLinkArmELb0ELb0E" in k for k in kernels), sorted(kernels)
+
+
+def test_bounded_two_link_group_kernels_in_the_basic_unit():
+    obj = os.path.join(AMD, "build", "group_two_link_bounded.o")
+    _need(obj)
+    kernels = [k for k in _kernel_metadata(obj) if "sqp_group_kernel" in k]
+    assert sorted(k.split("TwoLinkArmE")[1][:9] for k in kernels) == ["Lb0ELb1EL", "Lb1ELb0EL", "Lb1ELb0EL"], kernels
+    r = _rules(os.path.join(AMD, "Makefile"))
+    assert any("$(LANEFLAGS)" in l and "MMPC_GROUP_BOUNDED_UNIT" in l for l in r["build/group_two_link_bounded.o"])
+    assert "build/group_two_link_bounded.o" in open(os.path.join(AMD, "Makefile")).read().split("OBJS :=")[1].split("\n")[0]

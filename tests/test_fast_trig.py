@@ -22,16 +22,26 @@ extern "C" void fast_sincos_batch(const double* x, double* s, double* c, long n)
 """
 
 
-@pytest.fixture(scope="module")
-def lib(tmp_path_factory):
-    d = tmp_path_factory.mktemp("fast_trig")
+def _build(d, extra=()):
     src = d / "ft.cpp"
     src.write_text(SRC)
     so = d / "ft.so"
     # -ffp-contract=off: the host build rounds every product, the device build may contract; both stay within 1 ulp
-    subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-ffp-contract=off", "-I", CSRC, str(src), "-o", str(so)],
+    subprocess.run(["g++", "-O2", "-shared", "-fPIC", "-ffp-contract=off", *extra, "-I", CSRC, str(src), "-o", str(so)],
                    check=True)
     return ctypes.CDLL(str(so))
+
+
+@pytest.fixture(scope="module")
+def lib(tmp_path_factory):
+    return _build(tmp_path_factory.mktemp("fast_trig"))
+
+
+@pytest.fixture(scope="module")
+def devpath(tmp_path_factory):
+    """the device code path compiled for the host (no libm fallback), under UBSan that aborts on any report"""
+    return _build(tmp_path_factory.mktemp("fast_trig_dev"),
+                  ("-DMMPC_TRIG_DEVICE_PATH_ON_HOST", "-fsanitize=undefined", "-fno-sanitize-recover=all"))
 
 
 def _run(lib, x):
@@ -70,3 +80,21 @@ def test_special_values(lib):
     assert np.isnan(s[:3]).all() and np.isnan(c[:3]).all()
     assert s[3] == 0.0 and c[3] == 1.0
     assert s[4] == 1e-300 and s[5] == -1e-300 and c[4] == 1.0
+
+
+def test_huge_arguments_device_path_well_defined(devpath):
+    """a diverging iterate (|x| beyond 2^20 pi/2, up to 1e300): the device path returns NaN for both (the solver then
+    reports the instance non-finite) and never performs an out-of-range int conversion (UBSan would abort)"""
+    x = np.array([1647099.34, -2.0e6, 2.0 ** 31 * math.pi, -(2.0 ** 40) * 3.0, 1e15, -1e200, 1e300])
+    s, c = _run(devpath, x)
+    assert np.isnan(s).all() and np.isnan(c).all()
+    # up to the limit the device path is the one the default build uses
+    y = np.concatenate([np.random.default_rng(3).uniform(-1.6e6, 1.6e6, 2000), [1647099.32, -1647099.32]])
+    sd, cd = _run(devpath, y)
+    assert _ulps(sd, np.sin(y)).max() <= 1.0 and _ulps(cd, np.cos(y)).max() <= 1.0
+
+
+def test_huge_arguments_host_build_uses_libm(lib):
+    x = np.array([2.0e6, -3.3e9, 1e15, -1e200, 1e300])
+    s, c = _run(lib, x)
+    assert np.array_equal(s, np.array([math.sin(v) for v in x])) and np.array_equal(c, np.array([math.cos(v) for v in x]))

@@ -179,3 +179,85 @@ def test_multi_rccl_rejects_a_repeated_device(mmpc_mod, tmp_path):
     with pytest.raises(mmpc_mod.MmpcError):
         m.solve_batch_rccl(t(4, 4), t(4, 2), t(4, 30, 4), t(8), t(4, 184))
     m.close()
+
+
+def _rccl_vs_single(mmpc_mod, oracle, tmp_path, B, weights_rows=None, stride=None):
+    import torch
+    path = _multi_model(mmpc_mod, tmp_path)
+    N = 30
+    x0, up, tr = oracle.synth(11, 0, max(B, 1), N, 0.002)
+    x0, up, tr = x0[:B], up[:B], tr[:B]
+    d = lambda a: torch.tensor(np.ascontiguousarray(a), dtype=torch.float64, device="cuda:0")
+    w = d(np.array(WEIGHTS_CFG)) if weights_rows is None else d(weights_rows)
+    m = mmpc_mod.MultiSolver(path, [0])
+    V = torch.full((B, 30 * 6 + 4), 0.0, dtype=torch.float64, device="cuda:0")
+    st = torch.full((B,), -7, dtype=torch.int32, device="cuda:0")
+    it, kk = torch.zeros_like(st), torch.zeros(B, dtype=torch.float64, device="cuda:0")
+    m.solve_batch_rccl(d(x0), d(up), d(tr), w, V, st, it, kk, weights_stride=stride)
+    s = mmpc_mod.Solver(path)
+    V1, st1 = torch.zeros_like(V), torch.full_like(st, -7)
+    it1, kk1 = torch.zeros_like(it), torch.zeros_like(kk)
+    if B:
+        s.solve_batch(B, d(x0), d(up), d(tr), w, V1, st1, it1, kk1, weights_stride=stride or 0)
+    torch.cuda.synchronize()
+    m.close()
+    return (V, st, it, kk), (V1, st1, it1, kk1)
+
+
+@pytest.mark.parametrize("B", [0, 1])
+def test_multi_rccl_tiny_batches(B, mmpc_mod, oracle, tmp_path):
+    """B = 0 returns at once (nothing enqueued, outputs untouched); B = 1 is one shard of one instance: bit for bit the
+    single-handle solve"""
+    import torch
+    a, b = _rccl_vs_single(mmpc_mod, oracle, tmp_path, B)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    if B:
+        assert int(a[1][0]) == 0
+
+
+def test_multi_rccl_strided_weights_not_over_read(mmpc_mod, oracle, tmp_path):
+    """per-instance weights at weights_stride 11 > nx + 2 nu = 8 in a buffer of exactly (B - 1) 11 + 8 doubles: the
+    scatter sends the last row only up to its 8 entries, and the solve equals the single-handle solve"""
+    import torch
+    B = 37
+    rows = np.zeros((B - 1) * 11 + 8)
+    for i in range(B):
+        rows[i * 11:i * 11 + 8] = np.array(WEIGHTS_CFG) * (1.0 + 0.02 * i)
+    a, b = _rccl_vs_single(mmpc_mod, oracle, tmp_path, B, weights_rows=rows, stride=11)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    assert (a[1] == 0).all()
+
+
+def test_multi_rccl_rejects_a_short_weights_stride(mmpc_mod, tmp_path):
+    """weights_stride in (0, nx + 2 nu) is refused before any RCCL operation is issued"""
+    import torch
+    m = mmpc_mod.MultiSolver(_multi_model(mmpc_mod, tmp_path), [0])
+    t = lambda *s: torch.zeros(*s, dtype=torch.float64, device="cuda:0")
+    with pytest.raises(mmpc_mod.MmpcError, match="weights_stride"):
+        m.solve_batch_rccl(t(4, 4), t(4, 2), t(4, 30, 4), t(4 * 5), t(4, 184), weights_stride=5)
+    m.close()
+
+
+def test_multi_rccl_orders_after_the_callers_stream(mmpc_mod, oracle, tmp_path):
+    """inputs produced on a side stream the call is given (no host synchronisation in between): the first RCCL send
+    waits for that stream, so the solve sees the inputs; results equal the single-handle solve"""
+    import torch
+    path = _multi_model(mmpc_mod, tmp_path)
+    B, N = 256, 30
+    x0, up, tr = oracle.synth(13, 0, B, N, 0.002)
+    side = torch.cuda.Stream(device="cuda:0")
+    hx, hu, ht = (torch.tensor(a, dtype=torch.float64).pin_memory() for a in (x0, up, tr))
+    with torch.cuda.stream(side):
+        torch.cuda._sleep(20_000_000)   # the copies below land well after the call is made
+        dx, du, dt = (h.to("cuda:0", non_blocking=True) for h in (hx, hu, ht))
+        w = torch.tensor(WEIGHTS_CFG, dtype=torch.float64, device="cuda:0")
+        V = torch.zeros((B, 30 * 6 + 4), dtype=torch.float64, device="cuda:0")
+        st = torch.full((B,), -7, dtype=torch.int32, device="cuda:0")
+    m = mmpc_mod.MultiSolver(path, [0])
+    m.solve_batch_rccl(dx, du, dt, w, V, st, stream=side.cuda_stream)
+    torch.cuda.synchronize()
+    m.close()
+    ref = mmpc_mod.Solver(path).solve_batch_host(x0, up, tr, np.array(WEIGHTS_CFG))
+    assert np.array_equal(V.cpu().numpy(), ref["V"]) and (st.cpu().numpy() == 0).all()
