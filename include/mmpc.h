@@ -130,11 +130,11 @@ enum mmpc_hessian {
                                       an iteration whose KKT matrix is not positive definite on the null space takes
                                       the Gauss-Newton step.  Supported: nonlinear solves of models with second
                                       derivatives (the built-in 2-link arm and exo, SX-generated models) on the
-                                      RICCATI_GROUP solver (nx+nu < 16), unbounded or with control bounds (the held
-                                      controls are fixed in the exact QP; AUTO keeps Gauss-Newton for bounded
-                                      solves), and unbounded on the RICCATI (lane) solver; AUTO keeps Gauss-Newton
-                                      for the exo and on the lane solver.  State bounds, linear mode and any other
-                                      solve return MMPC_ERR_UNSUPPORTED */
+                                      RICCATI_GROUP solver (nx+nu < 16) and the RICCATI (lane) solver with its fp64
+                                      factor, unbounded or with control bounds (the held controls are fixed in the
+                                      exact QP; AUTO keeps Gauss-Newton for bounded solves); AUTO keeps Gauss-Newton
+                                      for the exo and on the lane solver.  State bounds, linear mode, the fp32
+                                      factor and any other solve return MMPC_ERR_UNSUPPORTED */
 };
 
 typedef struct mmpc_opts {
@@ -190,7 +190,7 @@ int mmpc_resolve_kkt_solver(const mmpc_handle* h, int64_t B, int32_t* solver);
 
 /* The Hessian (MMPC_HESSIAN_GAUSS_NEWTON or MMPC_HESSIAN_EXACT) a solve of B instances runs under the handle's
  * options; u_bounded = whether the solve passes control bounds (AUTO resolves control-bounded solves to
- * Gauss-Newton; an explicit EXACT is honoured with control bounds on RICCATI_GROUP).
+ * Gauss-Newton; an explicit EXACT is honoured with control bounds on RICCATI_GROUP and RICCATI).
  * MMPC_ERR_UNSUPPORTED when opts.hessian = EXACT cannot be honoured for that solve (state bounds, other solvers). */
 int mmpc_resolve_hessian(const mmpc_handle* h, int64_t B, int32_t u_bounded, int32_t* hessian);
 

@@ -640,18 +640,18 @@ int resolve_hessian(const mmpc_handle* h, int solver, bool u_bounded) {
         return MMPC_OK;
     });
     // control bounds (the projected SQP): EXACT fixes the held controls in the exact QP as in the Gauss-Newton one
-    // (group kernel); AUTO keeps Gauss-Newton there -- measured faster at cfg#2 with +-2 Nm (0.77 vs 0.91 ms: the
-    // exact solves take fewer iterations, but every re-solve after a hold repeats the costlier exact Riccati sweep,
-    // DESIGN.md 3b).  The lane kernel (round 4) takes EXACT for unbounded solves on request; AUTO there stays
+    // (group kernel; lane kernel since round 5); AUTO keeps Gauss-Newton there -- measured faster at cfg#2 with +-2 Nm
+    // (0.77 vs 0.91 ms: the exact solves take fewer iterations, but every re-solve after a hold repeats the costlier
+    // exact Riccati sweep).  The lane kernel (round 4) takes EXACT on request; AUTO there stays
     // Gauss-Newton (its backward sweep evaluates the model's Hessian per stage).
     const bool common = !h->x_bounded && !h->info.is_linear && !h->opts.factor_fp32;
     const bool group_ok = common && group_capable && solver == MMPC_KKT_RICCATI_GROUP;
-    const bool lane_ok = common && lane_capable && solver == MMPC_KKT_RICCATI && !u_bounded;
+    const bool lane_ok = common && lane_capable && solver == MMPC_KKT_RICCATI;
     if (want == MMPC_HESSIAN_EXACT) {
         if (!group_ok && !lane_ok)
             return fail(MMPC_ERR_UNSUPPORTED, "exact Hessian: needs a model with second derivatives, a Riccati "
-                                              "solver (RICCATI_GROUP; RICCATI without control bounds) and a "
-                                              "nonlinear solve without state bounds");
+                                              "solver (RICCATI_GROUP or RICCATI, fp64 factor) and a nonlinear solve "
+                                              "without state bounds");
         return MMPC_HESSIAN_EXACT;
     }
     return group_ok && dflt && !u_bounded ? MMPC_HESSIAN_EXACT : MMPC_HESSIAN_GAUSS_NEWTON;

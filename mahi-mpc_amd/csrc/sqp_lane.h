@@ -181,17 +181,19 @@ __device__ __forceinline__ gmem<double>* stage_ptr(double* wsb, int64_t k, int S
 // merit and iterates stay fp64, so every SQP iteration refines the fp32 step against fp64 residuals).
 // XB: state bounds, the primal-dual interior-point variant (oracle solve_one_ip; see sqp_group.h)
 // EXACT: the exact Lagrangian Hessian (IPOPT's default, CasADi nlp_hess_l at ModelGenerator.cpp:238; oracle
-// solve_one_riccati with ORACLE_HESS_EXACT): the backward step of stage k adds W_k = h sum_s lam_{k+1,NQ+s}
-// d^2 acc_s / d(x_k,u_k)^2 (Model::eval_hess at the iterate, lam the adjoint of this sweep) to H_ww, H_wx and the x
-// block of P~_k; a sweep whose H_ww is not positive definite is redone without W (the Gauss-Newton step)
+// solve_one_riccati / solve_one with ORACLE_HESS_EXACT): the backward step of stage k adds W_k = h sum_s
+// lam_{k+1,NQ+s} d^2 acc_s / d(x_k,u_k)^2 (Model::eval_hess at the iterate, lam the adjoint of this sweep) to H_ww,
+// H_wx and the x block of P~_k; a sweep whose H_ww is not positive definite is redone without W (the Gauss-Newton
+// step).  With control bounds (BOUNDED, round 5) the held controls are fixed in the exact stage QPs exactly as in
+// the Gauss-Newton ones (the hold rule acts on H_ww, H_wx, h_w after W is added).
 template <class Model, class FT = double, bool BOUNDED = false, bool XB = false, bool EXACT = false>
 // one wave per SIMD by design (P~ in LDS, ~40 KB per wave): telling the scheduler so lets it schedule for latency
 // rather than for a second wave's registers (cfg#3: 12.06 -> 11.94 ms)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_lane_kernel(SolveParams p,
                                                                                                  LaneWork lw) {
     static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
-    static_assert(!EXACT || (HasHess<Model>::value && std::is_same<FT, double>::value && !BOUNDED && !XB),
-                  "exact Hessian: unbounded fp64 solves of models with second derivatives");
+    static_assert(!EXACT || (HasHess<Model>::value && std::is_same<FT, double>::value && !XB),
+                  "exact Hessian: fp64 solves (unbounded or control-bounded) of models with second derivatives");
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
     constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)
     static_assert(NQ >= 0 && NA >= NQ, "x = [q; z] with qdot = z[0:NQ]");
@@ -497,10 +499,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void
         bool nft1 = false;
         // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
         double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
+        // exact-Hessian blocks in this iteration's sweeps; false after a sweep's exact QP was not positive definite:
+        // that sweep is redone and, with control bounds, every later QP solve of the iteration stays Gauss-Newton
+        // (oracle solve_one: gn_fallback)
+        bool useW = EXACT;
         #pragma unroll 1
         for (int pass = 0;; ++pass) {
             bool resolve = false;
-            bool useW = EXACT;   // exact-Hessian blocks in this sweep (false: the Gauss-Newton retry)
             #pragma unroll 1
             for (;;) {
             gmax = 0.0;

@@ -356,6 +356,23 @@ void oracle_set_exact_bounded(int on) { g_exact_bounded = on; }
  * whose multiplier -- the un-held QP gradient (H0 du + g0)_a at the solution -- points into the box is released as
  * well as a free control whose step crosses a bound held (Hintermueller, Ito & Kunisch 2003); two QP solves at the
  * first iteration, ORACLE_BOUND_PASSES later.  Off: holds are only added (the condensed and lane kernels). */
+/* test instrumentation: iterations whose exact-Hessian QP was not positive definite and took the Gauss-Newton step
+ * (solve_one and solve_one_riccati), summed over all threads since the last reset */
+static long long g_exact_fallbacks = 0;
+long long oracle_exact_fallbacks(int reset) {
+    long long v;
+#pragma omp atomic read
+    v = g_exact_fallbacks;
+    if (reset) {
+#pragma omp atomic write
+        g_exact_fallbacks = 0;
+    }
+    return v;
+}
+static void count_exact_fallback(void) {
+#pragma omp atomic
+    g_exact_fallbacks += 1;
+}
 static int g_bound_release = 0;
 void oracle_set_bound_release(int on) { g_bound_release = on; }
 
@@ -810,6 +827,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
                 if (!use_exact || gn_fallback) { fact_fail = 1; break; }
                 /* exact KKT matrix not positive definite: this iteration takes the Gauss-Newton step */
                 gn_fallback = 1;
+                count_exact_fallback();
                 if (has_b) {   /* the same pass again on the Gauss-Newton QP */
                     memcpy(s->H0, s->Hgn, sizeof(double) * M * M);
                     memcpy(s->g0, s->ggn, sizeof(double) * M);
@@ -1135,7 +1153,10 @@ static int solve_one_riccati(ws_t* s, double h, const double* x0, const double* 
                 for (int i = 0; i < K * K; ++i) Wk[i] *= h;
             }
         int rc = riccati_backward(s, traj, w, u_prev, use_exact);
-        if (rc != 0 && use_exact) rc = riccati_backward(s, traj, w, u_prev, 0);   /* not PD: Gauss-Newton step */
+        if (rc != 0 && use_exact) {   /* not PD: Gauss-Newton step */
+            count_exact_fallback();
+            rc = riccati_backward(s, traj, w, u_prev, 0);
+        }
         if (rc != 0) { status = ORACLE_FACTORIZATION_FAILED; break; }
         /* forward: du_k = K_k [dx_k; du_{k-1}] + kff_k, dx_{k+1} = A dx_k + B du_k + c_k */
         memset(s->dx, 0, sizeof(double) * NX);
@@ -1236,6 +1257,26 @@ static int solve_one_riccati(ws_t* s, double h, const double* x0, const double* 
  * complements lose positive definiteness to cancellation once Sigma reaches ~1e15 */
 #define IP_TOL_COMPL 1e-8
 #define IP_TAU 0.99
+
+/* barrier-parameter rule of solve_one_ip: 0 = IPOPT's monotone rule (shipped), 1 = Mehrotra predictor-corrector
+ * (round 5 experiment: an affine predictor solve, sigma = (mu_aff / mu)^3, a corrector solve with the second-order
+ * term on the same factor) */
+static int g_ip_rule = 0;
+void oracle_set_ip_rule(int rule) { g_ip_rule = rule; }
+
+/* solve with the Cholesky factor chol_solve left in the lower triangle of H */
+static void chol_resolve(int M, const double* L, double* b) {
+    for (int i = 0; i < M; ++i) {
+        double t = b[i];
+        for (int k = 0; k < i; ++k) t -= L[i * M + k] * b[k];
+        b[i] = t / L[i * M + i];
+    }
+    for (int i = M - 1; i >= 0; --i) {
+        double t = b[i];
+        for (int k = i + 1; k < M; ++k) t -= L[k * M + i] * b[k];
+        b[i] = t / L[i * M + i];
+    }
+}
 
 static double ip_push(double y, double l, double u) {
     const double pl = (l > -INFINITY) ? fmin(IP_PUSH * fmax(1.0, fabs(l)), (u < INFINITY) ? IP_PUSH * (u - l) : INFINITY) : 0.0;
@@ -1397,7 +1438,6 @@ static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_pre
                 if (fabs(t) > lmax) lmax = fabs(t);
             }
         /* condensed barrier Newton step: Hc = H + Sigma_U + G^T Sigma_X G, gc = g + b_U + G^T (b_X + Sigma_X d) */
-        for (int i = 0; i < S; ++i) tv[i] = bb[i] + sg[i] * s->d[NX + i];
         for (int a = 0; a < M; ++a) {
             for (int b = 0; b <= a; ++b) {
                 double t = 0.0;
@@ -1406,39 +1446,113 @@ static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_pre
                 if (b != a) s->H[b * M + a] += t;
             }
             s->H[a * M + a] += sg[S + a];
-            double t = s->g[a] + bb[S + a];
-            for (int i = 0; i < S; ++i) t += s->G[(size_t)i * M + a] * tv[i];
-            s->du[a] = -t;
         }
-        if (chol_solve(M, s->H, s->du) != 0) { status = ORACLE_FACTORIZATION_FAILED; break; }
-        memset(s->dx, 0, sizeof(double) * NX);
-        for (int k = 0; k < N; ++k)
-            for (int r = 0; r < NX; ++r) {
-                double t = s->c[k * NX + r];
-                for (int q = 0; q < NX; ++q) t += s->Ad[k * NX * NX + r * NX + q] * s->dx[k * NX + q];
-                for (int q = 0; q < NU; ++q) t += s->Bd[k * NX * NU + r * NU + q] * s->du[k * NU + q];
-                s->dx[(k + 1) * NX + r] = t;
+        /* rhs of the step for the barrier gradient bv (b of the monotone rule; the corrected b of Mehrotra's),
+         * solved with the factor of Hc (factored by the first call), expanded to dx and dy */
+        int fact_done = 0;
+        #define IP_SOLVE(bv)                                                                                        \
+            do {                                                                                                    \
+                for (int i = 0; i < S; ++i) tv[i] = (bv)[i] + sg[i] * s->d[NX + i];                                 \
+                for (int a = 0; a < M; ++a) {                                                                       \
+                    double t = s->g[a] + (bv)[S + a];                                                               \
+                    for (int i = 0; i < S; ++i) t += s->G[(size_t)i * M + a] * tv[i];                              \
+                    s->du[a] = -t;                                                                                  \
+                }                                                                                                   \
+                if (!fact_done) {                                                                                   \
+                    if (chol_solve(M, s->H, s->du) != 0) { fact_done = -1; break; }                                 \
+                    fact_done = 1;                                                                                  \
+                } else {                                                                                            \
+                    chol_resolve(M, s->H, s->du);                                                                   \
+                }                                                                                                   \
+                memset(s->dx, 0, sizeof(double) * NX);                                                              \
+                for (int k = 0; k < N; ++k)                                                                         \
+                    for (int r = 0; r < NX; ++r) {                                                                  \
+                        double t = s->c[k * NX + r];                                                                \
+                        for (int q = 0; q < NX; ++q) t += s->Ad[k * NX * NX + r * NX + q] * s->dx[k * NX + q];      \
+                        for (int q = 0; q < NU; ++q) t += s->Bd[k * NX * NU + r * NU + q] * s->du[k * NU + q];      \
+                        s->dx[(k + 1) * NX + r] = t;                                                                \
+                    }                                                                                               \
+                for (int i = 0; i < S; ++i) dy[i] = s->dx[NX + i];                                                  \
+                for (int a = 0; a < M; ++a) dy[S + a] = s->du[a];                                                   \
+            } while (0)
+        /* Mehrotra: the target mu and the corrected barrier gradient replace mu_b and bb of this iteration */
+        double* ccl = NULL;   /* corrector terms of the dual steps: mu_t - ds_aff dz_aff per lower / upper bound */
+        double* ccu = NULL;
+        if (g_ip_rule == 1 || g_ip_rule == 2) {
+            double* b0 = calloc((size_t)NY, sizeof(double));
+            IP_SOLVE(b0);   /* affine predictor: mu = 0 */
+            if (fact_done < 0) { free(b0); status = ORACLE_FACTORIZATION_FAILED; break; }
+            double ap = 1.0, ad = 1.0, sz = 0.0;
+            int m = 0;
+            for (int i = 0; i < NY; ++i) {
+                const double y = YV(i);
+                if (yl[i] > -INFINITY) {
+                    const double sl = y - yl[i], dz = -zl[i] - zl[i] / sl * dy[i];
+                    if (dy[i] < 0.0) ap = fmin(ap, -sl / dy[i]);
+                    if (dz < 0.0) ad = fmin(ad, -zl[i] / dz);
+                    sz += sl * zl[i];
+                    ++m;
+                }
+                if (yu[i] < INFINITY) {
+                    const double su = yu[i] - y, dz = -zu[i] + zu[i] / su * dy[i];
+                    if (dy[i] > 0.0) ap = fmin(ap, su / dy[i]);
+                    if (dz < 0.0) ad = fmin(ad, -zu[i] / dz);
+                    sz += su * zu[i];
+                    ++m;
+                }
             }
-        for (int i = 0; i < S; ++i) dy[i] = s->dx[NX + i];
-        for (int a = 0; a < M; ++a) dy[S + a] = s->du[a];
+            double saff = 0.0;
+            ccl = calloc((size_t)NY, sizeof(double));
+            ccu = calloc((size_t)NY, sizeof(double));
+            for (int i = 0; i < NY; ++i) {
+                const double y = YV(i);
+                if (yl[i] > -INFINITY) {
+                    const double sl = y - yl[i], dz = -zl[i] - zl[i] / sl * dy[i];
+                    saff += (sl + ap * dy[i]) * (zl[i] + ad * dz);
+                    ccl[i] = -dy[i] * dz;
+                }
+                if (yu[i] < INFINITY) {
+                    const double su = yu[i] - y, dz = -zu[i] + zu[i] / su * dy[i];
+                    saff += (su - ap * dy[i]) * (zu[i] + ad * dz);
+                    ccu[i] = dy[i] * dz;   /* -(ds_u)(dz_u), ds_u = -dy */
+                }
+            }
+            const double muc = m ? sz / m : 0.0, mua = m ? saff / m : 0.0;
+            const double sig = muc > 0.0 ? pow(mua / muc, 3.0) : 0.0;
+            mu_b = fmax(IP_TOL_COMPL / 20.0, fmin(sig * muc, IP_MU0));
+            for (int i = 0; i < NY; ++i) {
+                const double y = YV(i);
+                bb[i] = 0.0;
+                if (g_ip_rule == 2) ccl[i] = ccu[i] = 0.0;   /* probing only: no second-order correction */
+                if (yl[i] > -INFINITY) { ccl[i] += mu_b; bb[i] -= ccl[i] / (y - yl[i]); }
+                if (yu[i] < INFINITY) { ccu[i] += mu_b; bb[i] += ccu[i] / (yu[i] - y); }
+            }
+            free(b0);
+        }
+        IP_SOLVE(bb);
+        #undef IP_SOLVE
+        if (fact_done < 0) { status = ORACLE_FACTORIZATION_FAILED; break; }
         /* fraction to the boundary: primal alpha_max, dual alpha_z */
         const double tau = IP_TAU;
         double amax = 1.0, az = 1.0, dbar = 0.0;
         for (int i = 0; i < NY; ++i) {
             const double y = YV(i);
+            double bmu = 0.0;   /* barrier gradient at mu_b (the merit's), = bb for the monotone rule */
             if (yl[i] > -INFINITY) {
                 const double sl = y - yl[i];
                 if (dy[i] < 0.0) amax = fmin(amax, -tau * sl / dy[i]);
-                const double dz = mu_b / sl - zl[i] - zl[i] / sl * dy[i];
+                const double dz = (ccl ? ccl[i] : mu_b) / sl - zl[i] - zl[i] / sl * dy[i];
                 if (dz < 0.0) az = fmin(az, -tau * zl[i] / dz);
+                bmu -= mu_b / sl;
             }
             if (yu[i] < INFINITY) {
                 const double su = yu[i] - y;
                 if (dy[i] > 0.0) amax = fmin(amax, tau * su / dy[i]);
-                const double dz = mu_b / su - zu[i] + zu[i] / su * dy[i];
+                const double dz = (ccu ? ccu[i] : mu_b) / su - zu[i] + zu[i] / su * dy[i];
                 if (dz < 0.0) az = fmin(az, -tau * zu[i] / dz);
+                bmu += mu_b / su;
             }
-            dbar += 2.0 * bb[i] * dy[i];  /* J-scale directional derivative of -2 mu sum log s */
+            dbar += 2.0 * bmu * dy[i];  /* J-scale directional derivative of -2 mu sum log s */
         }
         /* l1-merit Armijo backtracking from alpha_max on J - 2 mu sum log s + nu |c|_1 */
         double nu_new = 4.0 * lmax + 1.0;
@@ -1484,13 +1598,17 @@ static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_pre
             if (dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * alpha * dphi + 1e-13 * noise) { accepted = 1; break; }
             alpha *= 0.5;
         }
-        if (!accepted) { status = ORACLE_LINESEARCH_FAILED; break; }
+        if (!accepted) { free(ccl); free(ccu); status = ORACLE_LINESEARCH_FAILED; break; }
         /* duals: z + alpha_z dz (dz at the old point), then the kappa_Sigma safeguard at the new point */
         for (int i = 0; i < NY; ++i) {
             const double y = YV(i);
-            if (yl[i] > -INFINITY) zl[i] += az * (mu_b / (y - yl[i]) - zl[i] - zl[i] / (y - yl[i]) * dy[i]);
-            if (yu[i] < INFINITY) zu[i] += az * (mu_b / (yu[i] - y) - zu[i] + zu[i] / (yu[i] - y) * dy[i]);
+            if (yl[i] > -INFINITY)
+                zl[i] += az * ((ccl ? ccl[i] : mu_b) / (y - yl[i]) - zl[i] - zl[i] / (y - yl[i]) * dy[i]);
+            if (yu[i] < INFINITY)
+                zu[i] += az * ((ccu ? ccu[i] : mu_b) / (yu[i] - y) - zu[i] + zu[i] / (yu[i] - y) * dy[i]);
         }
+        free(ccl);
+        free(ccu);
         memcpy(s->X, s->Xt, sizeof(double) * (N + 1) * NX);
         memcpy(s->U, s->Ut, sizeof(double) * M);
         for (int i = 0; i < NY; ++i) {
@@ -1504,7 +1622,7 @@ static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_pre
                 zu[i] = fmax(fmin(zu[i], IP_KAPPA_SIGMA * mu_b / su), mu_b / (IP_KAPPA_SIGMA * su));
             }
         }
-        mu_b = mu_next;
+        if (g_ip_rule == 0) mu_b = mu_next;
     }
 #undef YV
     for (int k = 0; k < N; ++k) {

@@ -127,6 +127,10 @@ int oracle_first_iter_filter_accepts(double J0, double c0, double Jt, double ct,
  * Cholesky, the default) or ORACLE_KKT_RICCATI (the Riccati recursion the HIP kernels run, same iterates) */
 enum { ORACLE_KKT_DENSE = 0, ORACLE_KKT_RICCATI = 1 };
 void oracle_set_kkt(int mode);
+/* barrier rule of the interior-point solve: 0 monotone (shipped), 1 Mehrotra predictor-corrector (experiment) */
+void oracle_set_ip_rule(int rule);
+/* test instrumentation: exact-Hessian iterations that fell back to the Gauss-Newton step since the last reset */
+long long oracle_exact_fallbacks(int reset);
 
 /* mmpc_opts.init_states for the following solves (process-wide): 0 = V as given, 1 = x_1..x_N start at x_0,
  * 2 = V taken as zero (MMPC_INIT_ZERO) */

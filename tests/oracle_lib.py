@@ -65,6 +65,9 @@ def lib():
         L.oracle_set_bound_release.argtypes = [C.c_int]
         L.oracle_nlp_hess.argtypes = [C.c_int, C.c_int, C.c_double, _dp, _dp, _dp, _dp, C.c_double, C.c_void_p, _dp]
         L.oracle_nlp_hess.restype = C.c_int
+        L.oracle_exact_fallbacks.argtypes = [C.c_int]
+        L.oracle_exact_fallbacks.restype = C.c_longlong
+        L.oracle_set_ip_rule.argtypes = [C.c_int]
         _lib = L
     return _lib
 
@@ -247,3 +250,15 @@ def _solve_batch(N, h, x0, u_prev, traj, weights, V, u_lb, u_ub, max_iter, tol_g
         nthreads)
     assert rc == 0
     return dict(V=V, status=st, iters=it, kkt=kkt, J=J)
+
+
+def exact_fallbacks(reset=True) -> int:
+    """exact-Hessian iterations of the oracle whose QP was not positive definite and took the Gauss-Newton step, since
+    the last reset (instrumentation for the tests that exercise that path)"""
+    return int(lib().oracle_exact_fallbacks(1 if reset else 0))
+
+
+def set_ip_rule(rule: int) -> None:
+    """barrier rule of the oracle's interior-point solve: 0 = IPOPT's monotone rule (the kernels'), 1 = Mehrotra
+    predictor-corrector, 2 = Mehrotra's probing without the corrector term (round-5 experiment)"""
+    lib().oracle_set_ip_rule(int(rule))

@@ -57,13 +57,70 @@ def test_group_exact_exo_vs_oracle(mmpc_mod, oracle, tmp_path):
 
 
 def test_exact_hessian_policy(mmpc_mod, tmp_path):
-    """AUTO keeps Gauss-Newton for the exo (more iterations exact) and on the lane kernel; EXACT with
-    control bounds on the lane kernel is refused (the projected lane solve is Gauss-Newton only)."""
+    """AUTO keeps Gauss-Newton for the exo (more iterations exact), on the lane kernel and for bounded
+    solves; an explicit EXACT is honoured on the lane kernel with and without control bounds (round 5), and refused
+    with the fp32 factor and with state bounds."""
     s = _solver(mmpc_mod, tmp_path, "exo_arm", 50)
     assert s.hessian_for(65536, False) == mmpc_mod.HESSIAN_GAUSS_NEWTON
     e = _solver(mmpc_mod, tmp_path, "exo_arm", 50, kkt_solver=2, hessian=mmpc_mod.HESSIAN_EXACT)
     assert e.hessian_for(64, False) == mmpc_mod.HESSIAN_EXACT
+    assert e.hessian_for(64, True) == mmpc_mod.HESSIAN_EXACT
+    f = _solver(mmpc_mod, tmp_path, "exo_arm", 50, kkt_solver=2, hessian=mmpc_mod.HESSIAN_EXACT, factor_fp32=1)
     with pytest.raises(mmpc_mod.MmpcError):
-        e.hessian_for(64, True)
+        f.hessian_for(64, False)
+    e.set_state_bounds([-np.inf] * 4 + [-1.5] * 4, [np.inf] * 4 + [1.5] * 4)
+    with pytest.raises(mmpc_mod.MmpcError):
+        e.hessian_for(64, False)
     t = _solver(mmpc_mod, tmp_path, "two_link_arm", 30, kkt_solver=2)
     assert t.hessian_for(64, False) == mmpc_mod.HESSIAN_GAUSS_NEWTON
+    assert _solver(mmpc_mod, tmp_path, "two_link_arm", 30, kkt_solver=2).hessian_for(64, True) == \
+        mmpc_mod.HESSIAN_GAUSS_NEWTON
+
+
+@pytest.mark.parametrize("model,N,B,ub", [("exo_arm", 50, 128, 0.5), ("exo_arm", 7, 65, 0.6), ("two_link_arm", 30, 128, 2.0)])
+def test_lane_exact_bounded_vs_oracle(model, N, B, ub, mmpc_mod, oracle, tmp_path):
+    """control bounds with the exact Hessian on the lane kernel (round 5) against the oracle's projected SQP with
+    ORACLE_HESS_EXACT (dense condensed, held controls fixed in the exact QP, Gauss-Newton for the rest of an iteration
+    whose exact QP is not positive definite); the bounds are active on most instances"""
+    om = oracle.EXO if model == "exo_arm" else oracle.TWO_LINK
+    w = W_EXO if model == "exo_arm" else np.array(WEIGHTS_CFG)
+    nu = 4 if model == "exo_arm" else 2
+    x0, up, tr = oracle.synth(20250213, 0, B, N, H, model=om)
+    lb, ub_ = np.full(nu, -ub), np.full(nu, ub)
+    s = _solver(mmpc_mod, tmp_path, model, N, kkt_solver=2, hessian=mmpc_mod.HESSIAN_EXACT,
+                init_states=mmpc_mod.INIT_ZERO)
+    assert s.kkt_solver_for(B) == 2 and s.hessian_for(B, True) == mmpc_mod.HESSIAN_EXACT
+    r = s.solve_batch_host(x0, up, tr, w, u_lb=lb, u_ub=ub_)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, u_lb=lb, u_ub=ub_, model=om, hessian=oracle.HESS_EXACT,
+                           init_states=2)
+    U = r["V"][:, :N * (nu + (8 if model == "exo_arm" else 4))].reshape(B, N, -1)[:, :, -nu:]
+    active = (np.abs(np.abs(U) - ub) < 1e-9).any(axis=(1, 2))
+    assert active.mean() > 0.5, active.mean()
+    assert (r["status"] == 0).all() and (o["status"] == 0).all()
+    _compare(r, o)
+    # the same KKT point as the bounded Gauss-Newton solve
+    g = _solver(mmpc_mod, tmp_path, model, N, kkt_solver=2, hessian=mmpc_mod.HESSIAN_GAUSS_NEWTON,
+                init_states=mmpc_mod.INIT_ZERO).solve_batch_host(x0, up, tr, w, u_lb=lb, u_ub=ub_)
+    assert _rel(r["V"], g["V"]).max() <= 1e-6
+
+
+@pytest.mark.parametrize("model,N,B,rscale,tscale", [("two_link_arm", 30, 256, 0.01, 20.0), ("exo_arm", 50, 128, 1.0, 20.0)])
+def test_lane_exact_gauss_newton_fallback(model, N, B, rscale, tscale, mmpc_mod, oracle, tmp_path):
+    """targets far from the initial state (x 20) and a small Delta-u weight: the multiplier-weighted term makes the
+    exact stage QP indefinite in some iterations (the oracle counts them), which then take the Gauss-Newton step --
+    the lane kernel's restart of the sweep without W, iteration for iteration the oracle's fallback"""
+    om = oracle.EXO if model == "exo_arm" else oracle.TWO_LINK
+    w = (W_EXO if model == "exo_arm" else np.array(WEIGHTS_CFG)).copy()
+    nx, nu = (8, 4) if model == "exo_arm" else (4, 2)
+    w[nx:nx + nu] *= rscale
+    x0, up, tr = oracle.synth(20250213, 0, B, N, H, model=om)
+    tr = np.ascontiguousarray(tr * tscale)
+    s = _solver(mmpc_mod, tmp_path, model, N, kkt_solver=2, hessian=mmpc_mod.HESSIAN_EXACT,
+                init_states=mmpc_mod.INIT_ZERO)
+    r = s.solve_batch_host(x0, up, tr, w)
+    oracle.exact_fallbacks(reset=True)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, model=om, hessian=oracle.HESS_EXACT, kkt=oracle.KKT_RICCATI,
+                           init_states=2)
+    assert oracle.exact_fallbacks() > 0   # the fallback path is exercised
+    assert (r["status"] == 0).all() and (o["status"] == 0).all()
+    _compare(r, o)
