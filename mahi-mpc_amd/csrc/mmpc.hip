@@ -469,62 +469,78 @@ __device__ __forceinline__ double affine_draw(double lo, double span, double u) 
     return lo + p;
 }
 
-// SURVEY.md 8d cfg#2 instance generator (identical recipe in oracle/ and tests/golden/)
+// SURVEY.md 8d cfg#2 instance generator (identical recipe in oracle/ and tests/golden/).  One thread per (instance,
+// stage) -- bench.py generates every step's instances inside its clock, and a thread per instance (30 sin / cos in
+// series, 960-byte strided stores) left all but 16 CUs idle for ~15 us at cfg#2: each thread redraws its instance's
+// three trajectory parameters (a few integer ops) and writes its stage's 32 bytes, contiguous across the wave; the
+// stage-0 thread also writes x0 and u_prev.  The phase argument is formed without FMA contraction, as the C oracle.
 __global__ __launch_bounds__(256) void synth_two_link_kernel(uint64_t seed, int64_t first, int64_t B, int N,
                                                              double h, double* x0, double* u_prev, double* traj) {
-    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (b >= B) return;
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= B * N) return;
+    const int64_t b = t / N;
+    const int k = (int)(t - b * N);
     const double PI = 3.14159265358979323846;
     const int64_t gi = first + b;
-    x0[b * 4 + 0] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 0));
-    x0[b * 4 + 1] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 1));
-    x0[b * 4 + 2] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 2));
-    x0[b * 4 + 3] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 3));
-    u_prev[b * 2 + 0] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 4));
-    u_prev[b * 2 + 1] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 5));
+    if (k == 0) {
+        x0[b * 4 + 0] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 0));
+        x0[b * 4 + 1] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 1));
+        x0[b * 4 + 2] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 2));
+        x0[b * 4 + 3] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 3));
+        u_prev[b * 2 + 0] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 4));
+        u_prev[b * 2 + 1] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 5));
+    }
     const double a = affine_draw(0.5, 0.5, unit_draw(seed, gi, 6));
     const double f = affine_draw(0.25, 0.75, unit_draw(seed, gi, 7));
     const double ph = affine_draw(0.0, 2.0 * PI, unit_draw(seed, gi, 8));
-    for (int k = 0; k < N; ++k) {
-        const double arg = 2.0 * PI * f * (k * h) + ph;
-        const double sv = a * sin(arg), cv = 2.0 * PI * f * a * cos(arg);
-        double* r = traj + (b * N + k) * 4;
-        r[0] = sv;
-        r[1] = -sv;
-        r[2] = cv;
-        r[3] = -cv;
+    double arg, cs;
+    {
+#pragma clang fp contract(off)
+        arg = 2.0 * PI * f * (k * h) + ph;
+        cs = 2.0 * PI * f * a;
     }
+    const double sv = a * sin(arg), cv = cs * cos(arg);
+    double* r = traj + t * 4;
+    r[0] = sv;
+    r[1] = -sv;
+    r[2] = cv;
+    r[3] = -cv;
 }
 
 // SURVEY.md 8d cfg#3 instance generator (identical recipe in oracle/mmpc_oracle.c): q, qd ~ U[-0.5, 0.5],
 // tau_prev ~ U[-1, 1], per joint a ~ U[0.1, 0.4], f ~ U[0.25, 1] Hz, phase ~ U[0, 2 pi];
-// r_k = [a sin(2 pi f t_k + phase); 2 pi f a cos(2 pi f t_k + phase)], t_k = k h.
+// r_k = [a sin(2 pi f t_k + phase); 2 pi f a cos(2 pi f t_k + phase)], t_k = k h.  One thread per (instance, stage),
+// as the cfg#2 generator.
 __device__ __forceinline__ double unit_draw_exo(uint64_t seed, int64_t index, int j) {
     const uint64_t v = splitmix64((seed + 0x3C6EF372FE94F82Aull) ^ splitmix64((uint64_t)index * 32ull + (uint64_t)j));
     return (double)(v >> 11) * 0x1.0p-53;
 }
 __global__ __launch_bounds__(256) void synth_exo_kernel(uint64_t seed, int64_t first, int64_t B, int N, double h,
                                                         double* x0, double* u_prev, double* traj) {
-    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (b >= B) return;
+    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (t >= B * N) return;
+    const int64_t b = t / N;
+    const int k = (int)(t - b * N);
     const double PI = 3.14159265358979323846;
     const int64_t gi = first + b;
-    double a[4], f[4], ph[4];
+    double* r = traj + t * 8;
     for (int j = 0; j < 4; ++j) {
-        x0[b * 8 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, j));
-        x0[b * 8 + 4 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, 4 + j));
-        u_prev[b * 4 + j] = affine_draw(-1.0, 2.0, unit_draw_exo(seed, gi, 8 + j));
-        a[j] = affine_draw(0.1, 0.3, unit_draw_exo(seed, gi, 12 + j));
-        f[j] = affine_draw(0.25, 0.75, unit_draw_exo(seed, gi, 16 + j));
-        ph[j] = affine_draw(0.0, 2.0 * PI, unit_draw_exo(seed, gi, 20 + j));
-    }
-    for (int k = 0; k < N; ++k) {
-        double* r = traj + (b * N + k) * 8;
-        for (int j = 0; j < 4; ++j) {
-            const double arg = 2.0 * PI * f[j] * (k * h) + ph[j];
-            r[j] = a[j] * sin(arg);
-            r[4 + j] = 2.0 * PI * f[j] * a[j] * cos(arg);
+        if (k == 0) {
+            x0[b * 8 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, j));
+            x0[b * 8 + 4 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, 4 + j));
+            u_prev[b * 4 + j] = affine_draw(-1.0, 2.0, unit_draw_exo(seed, gi, 8 + j));
         }
+        const double a = affine_draw(0.1, 0.3, unit_draw_exo(seed, gi, 12 + j));
+        const double f = affine_draw(0.25, 0.75, unit_draw_exo(seed, gi, 16 + j));
+        const double ph = affine_draw(0.0, 2.0 * PI, unit_draw_exo(seed, gi, 20 + j));
+        double arg, cs;
+        {
+#pragma clang fp contract(off)
+            arg = 2.0 * PI * f * (k * h) + ph;
+            cs = 2.0 * PI * f * a;
+        }
+        r[j] = a * sin(arg);
+        r[4 + j] = cs * cos(arg);
     }
 }
 
@@ -1211,10 +1227,10 @@ int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
     if (h->info.model_id == MMPC_MODEL_EXO_ARM)
-        synth_exo_kernel<<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        synth_exo_kernel<<<grid1d(B * N, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
             seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
     else
-        synth_two_link_kernel<<<grid1d(B, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        synth_two_link_kernel<<<grid1d(B * N, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
             seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;

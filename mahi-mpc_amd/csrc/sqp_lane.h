@@ -41,6 +41,9 @@
 #ifndef MMPC_LANE_FWD32
 #define MMPC_LANE_FWD32 1
 #endif
+#ifndef MMPC_LANE_WPE32
+#define MMPC_LANE_WPE32 1
+#endif
 
 namespace mmpc {
 
@@ -188,8 +191,12 @@ __device__ __forceinline__ gmem<double>* stage_ptr(double* wsb, int64_t k, int S
 // the Gauss-Newton ones (the hold rule acts on H_ww, H_wx, h_w after W is added).
 template <class Model, class FT = double, bool BOUNDED = false, bool XB = false, bool EXACT = false>
 // one wave per SIMD by design (P~ in LDS, ~40 KB per wave): telling the scheduler so lets it schedule for latency
-// rather than for a second wave's registers (cfg#3: 12.06 -> 11.94 ms)
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) void sqp_lane_kernel(SolveParams p,
+// rather than for a second wave's registers (cfg#3: 12.06 -> 11.94 ms).  The fp32-factor variant's P~ takes 20 KB, so
+// 8 waves fit a CU's LDS: MMPC_LANE_WPE32 = 2 (A/B builds) asks for 2 waves per SIMD there (256 registers)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(std::is_same<FT, float>::value ? MMPC_LANE_WPE32 : 1,
+                                                                    std::is_same<FT, float>::value ? MMPC_LANE_WPE32
+                                                                                                   : 1))) void
+sqp_lane_kernel(SolveParams p,
                                                                                                  LaneWork lw) {
     static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
     static_assert(!EXACT || (HasHess<Model>::value && std::is_same<FT, double>::value && !XB),
