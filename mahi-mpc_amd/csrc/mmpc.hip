@@ -1227,10 +1227,10 @@ int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
     if (h->info.model_id == MMPC_MODEL_EXO_ARM)
-        synth_exo_kernel<<<grid1d(B * N, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        synth_exo_kernel<<<grid1d(B * h->info.num_shooting_nodes, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
             seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
     else
-        synth_two_link_kernel<<<grid1d(B * N, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        synth_two_link_kernel<<<grid1d(B * h->info.num_shooting_nodes, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
             seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
