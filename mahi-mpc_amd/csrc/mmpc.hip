@@ -572,9 +572,10 @@ size_t workspace_bytes(const mmpc_model_info& mi, int nq, int64_t B, bool xb = t
            static_cast<size_t>(blocks) * sizeof(double);
 }
 
-size_t group_workspace_bytes(const mmpc_model_info& mi, int64_t B) {
-    return static_cast<size_t>(group_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes)) *
-           static_cast<size_t>(B) * sizeof(double);
+size_t group_workspace_bytes(const mmpc_model_info& mi, int64_t B) {   // the largest variant's (bounded or xb)
+    const int nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes;
+    const int per = std::max(group_ws_doubles(nx, nu, N, true, false), group_ws_doubles(nx, nu, N, false, true));
+    return static_cast<size_t>(per) * static_cast<size_t>(B) * sizeof(double);
 }
 size_t group_lds_bytes(const mmpc_model_info& mi, int nq, bool bounded = true, bool xb = false) {
     return static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, nq, mi.num_shooting_nodes, bounded && !xb,

@@ -26,19 +26,22 @@ constexpr int kGroupLanes = 16;
 constexpr int kGroupsPerWave = 4;
 
 // LDS doubles per instance.  The hold targets (bounded solves) and the linear-mode block are only allocated
-// when used: at cfg#2 that keeps a 4-instance workgroup at 38.8 KB, so 4 workgroups (one per SIMD) fit a CU's
-// 160 KB; with them 41 KB leaves one SIMD of every CU idle (measured: 0.78 vs 0.6x ms).
-// nq = kinematic rows of the model (sqp_lane.h a_mul); the stage blocks are h da/dq, h da/dz, h da/du.
-// xb: the interior-point variant (state bounds) adds z_l, z_u, Sigma, b, z_u - z_l per stage for (x_{k+1} | u_k).
+// when used: at cfg#2 that keeps a 4-instance workgroup at 39.0 KB (bounded: 39.75 KB), so 4 workgroups (one per
+// SIMD) fit a CU's 160 KB.  nq = kinematic rows of the model (sqp_lane.h a_mul); the stage blocks are h da/dq,
+// h da/dz, h da/du.  xb (the interior-point variant) adds nothing here since round 5: its per-stage z_l, z_u, Sigma,
+// b, z_u - z_l live in the HBM workspace (group_ws_doubles) -- in LDS they made 67.8 KB per workgroup at cfg#2, two
+// workgroups per CU, half the SIMDs idle and a 4096-instance batch in two rounds.
 // The d recursion prefetches two stages ahead without a clamp (d_recursion_dist): its reads of stages N and N + 1 of
-// sC, sFq and sFqd land in the arrays that follow each of them; the tail pad of 2 (nx - nq)^2 doubles keeps the last
-// one (sFqd) inside the instance's own block even when N nu < 2 (nx - nq) (exo shapes at N = 1), never in the next
-// group's block or past the end of the dynamic LDS.  The prefetched values are never used.
+// sC, sFq and sFqd land in the arrays that follow each of them.  When the arrays after sFqd (sFu, sR, ...) are
+// shorter than sFqd's overreach of 2 (nx - nq)^2 doubles (exo shapes at N = 1), a tail pad of that size keeps the read
+// inside the instance's own block, never in the next group's block or past the end of the dynamic LDS; otherwise no
+// pad (round 4 always padded: the control-bounded cfg#2 layout was then 40,960 B per workgroup).  The prefetched
+// values are never used.
 __host__ __device__ constexpr int group_lds_doubles(int nx, int nu, int nq, int N, bool bounded = true,
                                                    bool linear = true, bool xb = false) {
     return N * (3 * nx + (nx - nq) * (nq + (nx - nq) + nu) + 2 * nu) + 3 * (N + 1) * nx + (bounded ? N * nu : 0) +
-           (linear ? (nx - nq) * (nq + (nx - nq) + nu) + nx : 0) + (xb ? 5 * N * (nx + nu) : 0) +
-           2 * (nx - nq) * (nx - nq);
+           (linear ? (nx - nq) * (nq + (nx - nq) + nu) + nx : 0) +
+           (N * ((nx - nq) * nu + nx) >= 2 * (nx - nq) * (nx - nq) ? 0 : 2 * (nx - nq) * (nx - nq));
 }
 // exact Hessian (EXACT): per stage the x rows of W_k = h sum_s lam_{k+1,NQ+s} d^2 acc_s/d(x,u)^2 (nx x (nx+nu))
 // and its u-u block (nu x nu), written stage-parallel and read by the lane-distributed Riccati sweep
@@ -47,8 +50,11 @@ __host__ __device__ constexpr int group_hess_doubles(int nx, int nu) { return nx
 // solves only) the un-held rows [H_wx | -R | H_ww | h_w] of each stage QP, for the multipliers of the held controls.
 // The kernel strides instances by its own variant's size (unbounded solves: 1020 instead of 1560 doubles at cfg#2);
 // the host reserves the bounded size, the largest.
-__host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N, bool bounded = true) {
-    return N * nu * (nx + nu + 1) + N * group_hess_doubles(nx, nu) + (bounded ? N * nu * (nx + 2 * nu + 1) : 0);
+// xb (the interior-point variant, never with `bounded`): the per-stage z_l, z_u, Sigma, b, z_u - z_l of
+// (x_{k+1} | u_k) after the W blocks, in place of the bounded solves' rows.
+__host__ __device__ constexpr int group_ws_doubles(int nx, int nu, int N, bool bounded = true, bool xb = false) {
+    return N * nu * (nx + nu + 1) + N * group_hess_doubles(nx, nu) + (bounded ? N * nu * (nx + 2 * nu + 1) : 0) +
+           (xb ? 5 * N * (nx + nu) : 0);
 }
 
 struct GroupWork {
@@ -178,18 +184,20 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const sR = sFu + N * FU;                               // [N][NX]      targets r_k
     double* const sHold = sR + N * NX;                             // [N][NU]      bound a control is held at
     double* const sLin = sHold + (BOUNDED ? N * NU : 0);           // linear mode: Fq | Fqd | Fu | xdot
-    // interior point (XB): per stage k, y = (x_{k+1} | u_k) [NY]: duals z_l, z_u, Sigma, b, z_u - z_l
     constexpr int NY = NX + NU;
-    double* const sZl = sLin + (p.is_linear ? FQ + FD + FU + NX : 0);  // [N][NY]
-    double* const sZu = sZl + N * NY;
-    double* const sSg = sZu + N * NY;
-    double* const sBb = sSg + N * NY;
-    double* const sZg = sBb + N * NY;
-    double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N, BOUNDED);  // [N][NU][NS+1]
+    double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N, BOUNDED, XB);  // [N][NU][NS+1]
     constexpr int KZ = NX + NU, HW = group_hess_doubles(NX, NU);
     double* const wH = wK + N * NU * (NS + 1);  // EXACT: [N][HW] = W_k x rows [NX][KZ] | W_k uu block [NU][NU]
     constexpr int NR = NS + NU + 1;             // BOUNDED: [N][NU][NR] = un-held [H_wx | -R | H_ww | h_w] rows
     double* const wRel = wH + N * HW;
+    // interior point (XB): per stage k, y = (x_{k+1} | u_k) [NY]: duals z_l, z_u, Sigma, b, z_u - z_l -- in the HBM
+    // workspace after the W blocks (group_lds_doubles); the stage-parallel phases write them, the serial sweeps read
+    // them on other lanes after a workgroup fence
+    double* const sZl = wRel;  // [N][NY]
+    double* const sZu = sZl + N * NY;
+    double* const sSg = sZu + N * NY;
+    double* const sBb = sSg + N * NY;
+    double* const sZg = sBb + N * NY;
     const double* const trg = p.traj + ii * (int64_t)N * NX;
 
     const double* w = p.weights + ii * p.w_stride;
@@ -384,6 +392,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             cmpl0 = group_max(cmpl0);
             cmplmu = group_max(cmplmu);
             nonfinite |= !isfinite(lsum);
+            // Sigma, b, z_u - z_l of every stage (HBM workspace) visible to the other lanes' serial sweeps
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         }
         if (evalA) {
             J0 = group_sum(J0);

@@ -135,8 +135,8 @@ def test_hessian_policy(tmp_path, model_json, mmpc_mod):
     """mmpc_opts.hessian (include/mmpc.h) resolved without a GPU: AUTO = exact for unbounded nonlinear 2-link solves
     on the group kernel, Gauss-Newton for control-bounded (faster there) / state-bounded / linear /
     exo / lane-kernel solves; EXACT with control bounds is supported on the group kernel (the held controls fixed in
-    the exact QP); EXACT on the lane kernel for unbounded solves (round 4; the exo too); EXACT where unsupported
-    (state bounds, control bounds on the lane kernel, linear mode) is an API error."""
+    the exact QP); EXACT on the lane kernel (round 4; with control bounds since round 5; the exo too); EXACT where
+    unsupported (state bounds, the fp32 factor, linear mode) is an API error."""
     m = mmpc_mod
     s = m.Solver(model_json(N=30))
     assert s.hessian_for(4096) == m.HESSIAN_EXACT and s.hessian_for(64) == m.HESSIAN_EXACT
@@ -152,8 +152,10 @@ def test_hessian_policy(tmp_path, model_json, mmpc_mod):
     assert m.Solver(p, hessian=m.HESSIAN_EXACT).hessian_for(4096) == m.HESSIAN_EXACT
     p50 = m.write_model_json(str(tmp_path / "exo50.json"), "exo50", 8, 4, 2000, 50, model="exo_arm")
     assert m.Solver(p50, hessian=m.HESSIAN_EXACT).hessian_for(65536) == m.HESSIAN_EXACT    # lane kernel
-    with pytest.raises(m.MmpcError) as ei:                                # lane kernel, control bounds
-        m.Solver(p50, hessian=m.HESSIAN_EXACT).hessian_for(65536, u_bounded=True)
+    # lane kernel with control bounds: honoured since round 5 (held controls fixed in the exact stage QPs)
+    assert m.Solver(p50, hessian=m.HESSIAN_EXACT).hessian_for(65536, u_bounded=True) == m.HESSIAN_EXACT
+    with pytest.raises(m.MmpcError) as ei:                                # lane kernel, fp32 factor
+        m.Solver(p50, hessian=m.HESSIAN_EXACT, factor_fp32=1).hessian_for(65536)
     assert ei.value.code == -4
     with pytest.raises(m.MmpcError):                                      # linear mode
         m.Solver(model_json(N=30, name="lin2", is_linear=True), hessian=m.HESSIAN_EXACT).hessian_for(64)
