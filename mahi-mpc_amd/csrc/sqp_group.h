@@ -325,7 +325,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     // cfg#2 iteration, tools/alpha_stats.py) the next iteration skips phase A.  The trial point fma(1, d, v) is the
     // update's iterate and the sums run in phase A's order, so the values are phase A's bit for bit.  The old stage
     // blocks are dead once the directional derivative is formed; a rejected full step recomputes them in phase A.
-    constexpr bool FUSE_FWD = !XB;
+    // XB (round 5): the first trial is at alpha = alpha_max (fraction to the boundary) and the update's y is the same
+    // fma(alpha, dy, y) (ip_update), so the fused evaluation is again phase A's; the barrier terms (ip_terms) of phase
+    // A still run every iteration, after the dual update.
+    constexpr bool FUSE_FWD = true;
     bool fwd_ready = false;
     double J0n = 0.0, c1n = 0.0, cmaxn = 0.0;
     int nfn = 0;
@@ -1729,7 +1732,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
         bool jac_trial = false;
         for (int ls = 0; ls < 30; ++ls) {
             double Jt = 0.0, ct = 0.0, lt = 0.0;
-            jac_trial = FUSE_FWD && ls == 0;   // alpha = amax = 1 without state bounds
+            jac_trial = FUSE_FWD && ls == 0;   // alpha = amax (1 without state bounds)
             if (jac_trial) trial(std::true_type{}, Jt, ct, lt);
             else trial(std::false_type{}, Jt, ct, lt);
             Jt = group_sum(Jt);

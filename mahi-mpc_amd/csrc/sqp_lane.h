@@ -804,30 +804,33 @@ sqp_lane_kernel(SolveParams p,
                         yh[a] = std::is_same<FT, double>::value ? t * (double)il[a] : t / (double)Ld[a][a];
                     }
                     // [K_k | kff_k] = -L^-T [Y | yh]: kff (fp64) in the first NU slots of the K field, K (FT) after it
+                    // One column of K at a time, stored as soon as it is formed (the same expressions as a row-wise
+                    // back substitution, so the same values): 4 live gains instead of 48 (round 5 register diet)
                     {
-                        FT Kt[NU][NS];
+                        gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
+                        gmem<FT>* const kk = (gmem<FT>*)(kb + NU * 64) + lane;
                         double kh[NU];
 #pragma unroll
                         for (int a = NU - 1; a >= 0; --a) {
-#pragma unroll
-                            for (int j = 0; j < NS; ++j) {
-                                FT t = Y[a][j];
-#pragma unroll
-                                for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], Kt[q][j], t);
-                                Kt[a][j] = t * il[a];
-                            }
                             double t = yh[a];
 #pragma unroll
                             for (int q = a + 1; q < NU; ++q) t = fma(-(double)Ld[q][a], kh[q], t);
                             kh[a] = std::is_same<FT, double>::value ? t * (double)il[a] : t / (double)Ld[a][a];
                         }
-                        gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
-                        gmem<FT>* const kk = (gmem<FT>*)(kb + NU * 64) + lane;
 #pragma unroll
-                        for (int a = 0; a < NU; ++a) {
-                            kb[a * 64 + lane] = -kh[a];
+                        for (int a = 0; a < NU; ++a) kb[a * 64 + lane] = -kh[a];
 #pragma unroll
-                            for (int j = 0; j < NS; ++j) kk[(a * NS + j) * 64] = -Kt[a][j];
+                        for (int j = 0; j < NS; ++j) {
+                            FT kc[NU];
+#pragma unroll
+                            for (int a = NU - 1; a >= 0; --a) {
+                                FT t = Y[a][j];
+#pragma unroll
+                                for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], kc[q], t);
+                                kc[a] = t * il[a];
+                            }
+#pragma unroll
+                            for (int a = 0; a < NU; ++a) kk[(a * NS + j) * 64] = -kc[a];
                         }
                     }
                     if (k == 0) break;  // s_0 = 0: P~_0 is never used

@@ -28,6 +28,7 @@ ap.add_argument("--horizon", type=int, default=None)
 ap.add_argument("--kkt", type=int, default=0, help="kkt_solver (0 auto, 1 condensed, 2 riccati)")
 ap.add_argument("--u-bound", type=float, default=None, help="control bounds |u| <= U (projected SQP)")
 ap.add_argument("--hessian", type=int, default=0, help="mmpc_opts.hessian (0 auto, 1 Gauss-Newton, 2 exact)")
+ap.add_argument("--x-bound", type=float, default=None, help="state bounds |qdot| <= X (interior point)")
 a = ap.parse_args()
 exo = a.config == "cfg3"
 B = a.batch or (65536 if exo else 4096)
@@ -37,6 +38,8 @@ L = mmpc.lib()
 L.mmpc_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
 path = mmpc.write_model_json("/tmp/mmpc_phase.json", "phase", nx, nu, 2000, N)
 s = mmpc.Solver(path, kkt_solver=a.kkt, hessian=a.hessian)
+if a.x_bound is not None:
+    s.set_state_bounds([-np.inf] * (nx // 2) + [-a.x_bound] * (nx // 2), [np.inf] * (nx // 2) + [a.x_bound] * (nx // 2))
 NAMES_GROUP = ["load", "A:evals(parallel)", "B:d+adjoint(+riccati if not DIST)", "riccati(DIST)+mu",
                "C:step(serial)+dJ", "D:line_search", "after_loop", "writeback", "update(loop top)", "check"]
 if a.kkt == 3:
@@ -62,7 +65,7 @@ L.mmpc_debug_phase_cycles(buf, 1)
 cyc = np.array(buf[:10], dtype=np.float64)
 waves = buf[15]
 iters = it.cpu().numpy()
-out = {"config": a.config, "u_bound": a.u_bound, "hessian": s.hessian_for(B, a.u_bound is not None), "waves": int(waves), "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
+out = {"config": a.config, "u_bound": a.u_bound, "x_bound": a.x_bound, "hessian": s.hessian_for(B, a.u_bound is not None), "waves": int(waves), "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
        "cycles_per_wave": float(cyc.sum() / waves),
        "per_phase_cycles_per_wave_iteration": {n: float(c / waves / (iters.mean() + 1)) for n, c in zip(NAMES, cyc)},
        "share": {n: float(c / cyc.sum()) for n, c in zip(NAMES, cyc)}}
