@@ -469,82 +469,114 @@ __device__ __forceinline__ double affine_draw(double lo, double span, double u) 
     return lo + p;
 }
 
-// SURVEY.md 8d cfg#2 instance generator (identical recipe in oracle/ and tests/golden/).  One thread per (instance,
-// stage) -- bench.py generates every step's instances inside its clock, and a thread per instance (30 sin / cos in
-// series, 960-byte strided stores) left all but 16 CUs idle for ~15 us at cfg#2: each thread redraws its instance's
-// three trajectory parameters (a few integer ops) and writes its stage's 32 bytes, contiguous across the wave; the
-// stage-0 thread also writes x0 and u_prev.  The phase argument is formed without FMA contraction, as the C oracle.
-__global__ __launch_bounds__(256) void synth_two_link_kernel(uint64_t seed, int64_t first, int64_t B, int N,
-                                                             double h, double* x0, double* u_prev, double* traj) {
-    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (t >= B * N) return;
-    const int64_t b = t / N;
-    const int k = (int)(t - b * N);
-    const double PI = 3.14159265358979323846;
-    const int64_t gi = first + b;
-    if (k == 0) {
-        x0[b * 4 + 0] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 0));
-        x0[b * 4 + 1] = affine_draw(-PI / 4, PI / 2, unit_draw(seed, gi, 1));
-        x0[b * 4 + 2] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 2));
-        x0[b * 4 + 3] = affine_draw(-1.0, 2.0, unit_draw(seed, gi, 3));
-        u_prev[b * 2 + 0] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 4));
-        u_prev[b * 2 + 1] = affine_draw(-5.0, 10.0, unit_draw(seed, gi, 5));
-    }
-    const double a = affine_draw(0.5, 0.5, unit_draw(seed, gi, 6));
-    const double f = affine_draw(0.25, 0.75, unit_draw(seed, gi, 7));
-    const double ph = affine_draw(0.0, 2.0 * PI, unit_draw(seed, gi, 8));
-    double arg, cs;
-    {
-#pragma clang fp contract(off)
-        arg = 2.0 * PI * f * (k * h) + ph;
-        cs = 2.0 * PI * f * a;
-    }
-    const double sv = a * sin(arg), cv = cs * cos(arg);
-    double* r = traj + t * 4;
-    r[0] = sv;
-    r[1] = -sv;
-    r[2] = cv;
-    r[3] = -cv;
-}
+// SURVEY.md 8d instance generators (identical recipes in oracle/mmpc_oracle.c and tests/golden/).  bench.py generates
+// every step's instances inside its clock, so they are built for throughput: a 256-thread block takes
+// I = max(1, 256 / N) instances; its threads first form the instances' unit draws (each exactly once, into LDS; the
+// x0 / u_prev draws go straight to memory), then one thread per (instance, stage) forms that stage's targets (sin /
+// cos of the phase, stores contiguous across the block).  Round 4 ran one thread per instance (30-50 sin / cos in
+// series, strided stores, 16 CUs busy at cfg#2: 12.3 us per batch); a first round-5 version redrew every instance's
+// parameters in each stage's thread (5.2 us at cfg#2 but 165 us at cfg#3: the 64-bit multiplies of splitmix64).
+// The phase argument is formed without FMA contraction, as the C oracle.
+constexpr int kSynthThreads = 256;
 
-// SURVEY.md 8d cfg#3 instance generator (identical recipe in oracle/mmpc_oracle.c): q, qd ~ U[-0.5, 0.5],
-// tau_prev ~ U[-1, 1], per joint a ~ U[0.1, 0.4], f ~ U[0.25, 1] Hz, phase ~ U[0, 2 pi];
-// r_k = [a sin(2 pi f t_k + phase); 2 pi f a cos(2 pi f t_k + phase)], t_k = k h.  One thread per (instance, stage),
-// as the cfg#2 generator.
-__device__ __forceinline__ double unit_draw_exo(uint64_t seed, int64_t index, int j) {
-    const uint64_t v = splitmix64((seed + 0x3C6EF372FE94F82Aull) ^ splitmix64((uint64_t)index * 32ull + (uint64_t)j));
-    return (double)(v >> 11) * 0x1.0p-53;
-}
-__global__ __launch_bounds__(256) void synth_exo_kernel(uint64_t seed, int64_t first, int64_t B, int N, double h,
-                                                        double* x0, double* u_prev, double* traj) {
-    const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (t >= B * N) return;
-    const int64_t b = t / N;
-    const int k = (int)(t - b * N);
+// cfg#2: q ~ U[-pi/4, pi/4], qdot ~ U[-1, 1], u_prev ~ U[-5, 5]; a ~ U[0.5, 1], f ~ U[0.25, 1] Hz, phase ~ U[0, 2 pi];
+// r_k = [a sin(2 pi f t_k + phase), -a sin(.), 2 pi f a cos(.), -2 pi f a cos(.)], t_k = k h
+__global__ __launch_bounds__(kSynthThreads) void synth_two_link_kernel(uint64_t seed, int64_t first, int64_t B, int N,
+                                                                       double h, double* x0, double* u_prev,
+                                                                       double* traj) {
+    constexpr int ND = 9;   // draws per instance: x0 (4), u_prev (2), a, f, phase
+    __shared__ double dr[kSynthThreads][3];
+    const int I = N < kSynthThreads ? kSynthThreads / N : 1;
+    const int64_t b0 = (int64_t)blockIdx.x * I;
     const double PI = 3.14159265358979323846;
-    const int64_t gi = first + b;
-    double* r = traj + t * 8;
-    for (int j = 0; j < 4; ++j) {
-        if (k == 0) {
-            x0[b * 8 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, j));
-            x0[b * 8 + 4 + j] = affine_draw(-0.5, 1.0, unit_draw_exo(seed, gi, 4 + j));
-            u_prev[b * 4 + j] = affine_draw(-1.0, 2.0, unit_draw_exo(seed, gi, 8 + j));
-        }
-        const double a = affine_draw(0.1, 0.3, unit_draw_exo(seed, gi, 12 + j));
-        const double f = affine_draw(0.25, 0.75, unit_draw_exo(seed, gi, 16 + j));
-        const double ph = affine_draw(0.0, 2.0 * PI, unit_draw_exo(seed, gi, 20 + j));
+    for (int t = threadIdx.x; t < I * ND; t += kSynthThreads) {
+        const int i = t / ND, j = t - i * ND;
+        const int64_t b = b0 + i;
+        if (b >= B) continue;
+        const double u = unit_draw(seed, first + b, j);
+        if (j < 2) x0[b * 4 + j] = affine_draw(-PI / 4, PI / 2, u);
+        else if (j < 4) x0[b * 4 + j] = affine_draw(-1.0, 2.0, u);
+        else if (j < 6) u_prev[b * 2 + j - 4] = affine_draw(-5.0, 10.0, u);
+        else if (j == 6) dr[i][0] = affine_draw(0.5, 0.5, u);
+        else if (j == 7) dr[i][1] = affine_draw(0.25, 0.75, u);
+        else dr[i][2] = affine_draw(0.0, 2.0 * PI, u);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < I * N; t += kSynthThreads) {
+        const int i = t / N, k = t - i * N;
+        const int64_t b = b0 + i;
+        if (b >= B) continue;
+        const double a = dr[i][0], f = dr[i][1], ph = dr[i][2];
         double arg, cs;
         {
 #pragma clang fp contract(off)
             arg = 2.0 * PI * f * (k * h) + ph;
             cs = 2.0 * PI * f * a;
         }
-        r[j] = a * sin(arg);
-        r[4 + j] = cs * cos(arg);
+        double sn, cn;
+        sincos(arg, &sn, &cn);   // one argument reduction for both (the device library's sin and cos values)
+        const double sv = a * sn, cv = cs * cn;
+        double* r = traj + (b * N + k) * 4;
+        r[0] = sv;
+        r[1] = -sv;
+        r[2] = cv;
+        r[3] = -cv;
+    }
+}
+
+// cfg#3: q, qd ~ U[-0.5, 0.5], tau_prev ~ U[-1, 1], per joint a ~ U[0.1, 0.4], f ~ U[0.25, 1] Hz, phase ~ U[0, 2 pi];
+// r_k = [a sin(2 pi f t_k + phase); 2 pi f a cos(2 pi f t_k + phase)], t_k = k h
+__device__ __forceinline__ double unit_draw_exo(uint64_t seed, int64_t index, int j) {
+    const uint64_t v = splitmix64((seed + 0x3C6EF372FE94F82Aull) ^ splitmix64((uint64_t)index * 32ull + (uint64_t)j));
+    return (double)(v >> 11) * 0x1.0p-53;
+}
+__global__ __launch_bounds__(kSynthThreads) void synth_exo_kernel(uint64_t seed, int64_t first, int64_t B, int N,
+                                                                  double h, double* x0, double* u_prev, double* traj) {
+    constexpr int ND = 24;   // draws per instance: x0 (8), u_prev (4), per joint a, f, phase (12)
+    __shared__ double dr[kSynthThreads][12];
+    const int I = N < kSynthThreads ? kSynthThreads / N : 1;
+    const int64_t b0 = (int64_t)blockIdx.x * I;
+    const double PI = 3.14159265358979323846;
+    for (int t = threadIdx.x; t < I * ND; t += kSynthThreads) {
+        const int i = t / ND, j = t - i * ND;
+        const int64_t b = b0 + i;
+        if (b >= B) continue;
+        const double u = unit_draw_exo(seed, first + b, j);
+        if (j < 8) x0[b * 8 + j] = affine_draw(-0.5, 1.0, u);
+        else if (j < 12) u_prev[b * 4 + j - 8] = affine_draw(-1.0, 2.0, u);
+        else if (j < 16) dr[i][j - 12] = affine_draw(0.1, 0.3, u);
+        else if (j < 20) dr[i][j - 12] = affine_draw(0.25, 0.75, u);
+        else dr[i][j - 12] = affine_draw(0.0, 2.0 * PI, u);
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < I * N; t += kSynthThreads) {
+        const int i = t / N, k = t - i * N;
+        const int64_t b = b0 + i;
+        if (b >= B) continue;
+        double* r = traj + (b * N + k) * 8;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double a = dr[i][j], f = dr[i][4 + j], ph = dr[i][8 + j];
+            double arg, cs;
+            {
+#pragma clang fp contract(off)
+                arg = 2.0 * PI * f * (k * h) + ph;
+                cs = 2.0 * PI * f * a;
+            }
+            double sn, cn;
+            sincos(arg, &sn, &cn);
+            r[j] = a * sn;
+            r[4 + j] = cs * cn;
+        }
     }
 }
 
 inline unsigned grid1d(int64_t B, int threads) { return static_cast<unsigned>((B + threads - 1) / threads); }
+// blocks of the instance generators: I = max(1, kSynthThreads / N) instances per block
+inline unsigned synth_blocks(int64_t B, int N) {
+    const int64_t I = N < kSynthThreads ? kSynthThreads / N : 1;
+    return static_cast<unsigned>((B + I - 1) / I);
+}
 
 // Calls f((Model*)nullptr) for the model compiled into this library under model_id.
 template <class F>
@@ -1228,10 +1260,12 @@ int mmpc_synth_batch(mmpc_handle* h, uint64_t seed, int64_t first_index, int64_t
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
     if (h->info.model_id == MMPC_MODEL_EXO_ARM)
-        synth_exo_kernel<<<grid1d(B * h->info.num_shooting_nodes, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        synth_exo_kernel<<<synth_blocks(B, h->info.num_shooting_nodes), kSynthThreads, 0,
+                           reinterpret_cast<hipStream_t>(stream)>>>(
             seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
     else
-        synth_two_link_kernel<<<grid1d(B * h->info.num_shooting_nodes, 256), 256, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        synth_two_link_kernel<<<synth_blocks(B, h->info.num_shooting_nodes), kSynthThreads, 0,
+                                reinterpret_cast<hipStream_t>(stream)>>>(
             seed, first_index, B, h->info.num_shooting_nodes, h->info.step_size, x0, u_prev, traj);
     MMPC_HIP(hipGetLastError());
     return MMPC_OK;
