@@ -158,13 +158,17 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     [[maybe_unused]] const int lane0 = threadIdx.x;
     MMPC_PHASE_DECL
     const int gbase = gi * G;  // first lane of this instance's group
-    const int64_t inst = (int64_t)blockIdx.x * kGroupsPerWave + gi;
-    const bool valid = inst < p.B;
+    // slot of this group in the launch: the instance itself, or (resume launch, p.tail_idx) an entry of the lane
+    // kernel's hand-over list
+    const int64_t slot = (int64_t)blockIdx.x * p.gpw + gi;
+    const bool resume = p.tail_idx != nullptr;
+    const bool valid = gi < p.gpw && slot < (resume ? (int64_t)min(*p.tail_count, p.tail_slots) : p.B);
     // a group past the end of the batch (the last wave of a B not divisible by 4) leaves at once: no group reads
     // another group's lanes (row_bcast and the group reductions stay inside the 16-lane row) or LDS block, so
     // nothing else in the wave needs it, and it issues no memory access at all (round 4 had those groups run on
     // aliased to instance 0 and masked by `done`, which made every store's masking a correctness condition)
     if (!valid) return;
+    const int64_t inst = resume ? (int64_t)p.tail_idx[slot] : slot;
     const int64_t ii = inst;
     const int N = p.N;
     const int NV = NX * (N + 1) + NU * N;
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const sHold = sR + N * NX;                             // [N][NU]      bound a control is held at
     double* const sLin = sHold + (BOUNDED ? N * NU : 0);           // linear mode: Fq | Fqd | Fu | xdot
     constexpr int NY = NX + NU;
-    double* const wK = gw.ws + ii * (int64_t)group_ws_doubles(NX, NU, N, BOUNDED, XB);  // [N][NU][NS+1]
+    double* const wK = gw.ws + slot * (int64_t)group_ws_doubles(NX, NU, N, BOUNDED, XB);  // [N][NU][NS+1]
     constexpr int KZ = NX + NU, HW = group_hess_doubles(NX, NU);
     double* const wH = wK + N * NU * (NS + 1);  // EXACT: [N][HW] = W_k x rows [NX][KZ] | W_k uu block [NU][NU]
     constexpr int NR = NS + NU + 1;             // BOUNDED: [N][NU][NR] = un-held [H_wx | -R | H_ww | h_w] rows
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     __builtin_amdgcn_wave_barrier();
     int status = ST_MAX_ITER;
     int it = 0;
-    double kkt = 0.0, mu = 0.0, pg_prev = INFINITY;
+    double kkt = 0.0, mu = resume ? p.tail_mu[slot] : 0.0, pg_prev = INFINITY;
     bool done = !valid;
     // FUSE_FWD: the line search's alpha = 1 trial evaluates the model with its Jacobian and writes everything phase A
     // computes at that point (F_k, c_k, the stage blocks; J, |c|_1, max|c|); when the full step is accepted (every
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double J0n = 0.0, c1n = 0.0, cmaxn = 0.0;
     int nfn = 0;
     MMPC_PHASE(0);
-    for (it = 0; !done; ++it) {
+    for (it = resume ? p.tail_it[slot] : 0; !done; ++it) {
         MMPC_PHASE(8);
         __builtin_amdgcn_wave_barrier();
         // ---- A. stage-parallel: F_k, A_k/B_k blocks, defects, merit value ----

@@ -953,6 +953,19 @@ sqp_lane_kernel(SolveParams p,
                     done = true;
                     break;
                 }
+                // tail hand-over (unbounded solves): the instance continues in a 16-lane resume launch from this
+                // iterate, iteration count and merit weight -- the wave no longer waits for it
+                if (!BOUNDED && !XB && p.tail_cap > 0 && it == p.tail_cap) {
+                    const int slot = atomicAdd(p.tail_count, 1);
+                    if (slot < p.tail_slots) {
+                        p.tail_idx[slot] = (int32_t)inst;
+                        p.tail_it[slot] = it;
+                        p.tail_mu[slot] = mu;
+                        status = ST_HANDED_OVER;
+                        done = true;
+                        break;
+                    }
+                }
                 if (BOUNDED) pg_prev = gmax;
                 // barrier update for the next iteration (IPOPT monotone rule, lagged; oracle solve_one_ip)
                 if (XB && fmax(fmax(0.5 * gmax, cmax), cmplmu) <= kIpKappaEps * mub)

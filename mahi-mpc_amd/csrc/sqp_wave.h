@@ -61,7 +61,20 @@ struct SolveParams {
     double* trace;  // debug: [B][max_iter+1][8] per-iteration diagnostics, or nullptr
     int init_hold;  // mmpc_opts.init_states == MMPC_INIT_HOLD_X0: x_1..x_N start at x_0 (controls as given)
     int init_zero;  // mmpc_opts.init_states == MMPC_INIT_ZERO: V is not read, the iterate starts at 0 (x_0 pinned)
+    // iteration-tail hand-over, lane kernel -> 16-lane kernel (DESIGN.md 4b "tail hand-over"): at the stop test of
+    // iteration tail_cap an unconverged lane-kernel instance claims a slot of the list (atomic on tail_count) and
+    // stops with its iterate written back; a 16-lane resume launch over the list continues it from there, with the
+    // same iteration count and l1-merit weight.  Instances beyond tail_slots keep iterating in the lane kernel.
+    int tail_cap;          // 0: no hand-over
+    int tail_slots;        // capacity of the list
+    int32_t* tail_count;   // [1] claims (may exceed tail_slots)
+    int32_t* tail_idx;     // [tail_slots] instance; in a 16-lane launch, non-null = resume launch over the list
+    int32_t* tail_it;      // [tail_slots] iteration whose stop test failed
+    double* tail_mu;       // [tail_slots] l1-merit penalty weight
+    int gpw;               // 16-lane kernel: instance groups per wave of this launch (kGroupsPerWave, or fewer)
 };
+// instance status while handed over (never returned: the resume launch overwrites it)
+constexpr int ST_HANDED_OVER = 6;
 
 enum {
     ST_CONVERGED = 0,
