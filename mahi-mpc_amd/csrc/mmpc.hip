@@ -80,6 +80,7 @@ struct mmpc_handle {
     // iteration-tail hand-over: cap override from MMPC_TAIL_CAP at creation (-1: the default policy),
     // compute units of the device (slots of the resume launch)
     int tail_cap_env = -1;
+    int tail_rounds_env = -1;   // MMPC_TAIL_ROUNDS: rounds of resume workgroups (-1: 4)
     int cu_count = 0;
     // state bounds of x_1..x_N (JSON x_min/x_max, or mmpc_set_state_bounds); copied into each launch's arguments
     double x_lb[16], x_ub[16];
@@ -737,7 +738,7 @@ int ensure_workspace_bytes(mmpc_handle* h, size_t bytes, double** out) {
     return MMPC_OK;
 }
 // iteration-tail hand-over list after the solver workspace: [count | pad][idx: slots x i32][it: slots x i32][mu]
-constexpr int kTailMaxSlots = 4096;
+constexpr int kTailMaxSlots = 65536;
 constexpr size_t kTailBytes = 256 + static_cast<size_t>(kTailMaxSlots) * 16;
 size_t solver_workspace_bytes(const mmpc_handle* h, int64_t B) {
     return (std::max(workspace_bytes(h->info, h->nq, B), group_workspace_bytes(h->info, B)) + 255) / 256 * 256;
@@ -751,20 +752,22 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
 // Iteration-tail hand-over of a lane-kernel solve: the lane kernel's wave runs until its slowest lane
 // converges (cfg#3: 1 % of the instances need a 5th iteration, and the waves holding them set the kernel time), so
 // instances still unconverged at the stop test of iteration `cap` continue in a 16-lane resume launch, whose
-// per-iteration latency is ~5x lower (exo N = 24, B = 256: 0.30 vs 1.68 ms). Unbounded fp64 nonlinear solves of models
-// the 16-lane kernel runs (nx + nu < 16), without the diagnostic trace. cap: 4 (Gauss-Newton) / 5 (exact Hessian:
-// one more typical iteration), MMPC_TAIL_CAP overrides (0 = off). slots: what one resume wave of workgroups holds
-// (groups per workgroup gpw with <= 64 KB of LDS, up to 4 one-wave workgroups per CU).
+// per-iteration latency is ~5x lower (exo N = 24, B = 256: 0.30 vs 1.68 ms). Unbounded nonlinear solves of models
+// the 16-lane kernel runs (nx + nu < 16), without the diagnostic trace; a solve with the fp32 Riccati factor continues
+// its tail with the fp64 factor (precision escalation: same stop test, same iterate). cap: 4 (Gauss-Newton and exact
+// Hessian; 3 hands over too many: cfg#3 12.8 ms), MMPC_TAIL_CAP overrides (0 = off). slots: four rounds of resume
+// workgroups (groups per workgroup gpw with <= 64 KB of LDS, up to 4 one-wave workgroups per CU per round),
+// MMPC_TAIL_ROUNDS overrides.
 struct TailPlan {
     int cap = 0, slots = 0, gpw = 1;
     size_t lds = 0;
 };
-TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded, int hess) {
+TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded) {
     TailPlan t;
     const mmpc_model_info& mi = h->info;
-    if (bounded || p.x_bounded || h->opts.factor_fp32 || mi.is_linear || p.trace || h->cu_count <= 0) return t;
+    if (bounded || p.x_bounded || mi.is_linear || p.trace || h->cu_count <= 0) return t;
     if (mi.num_x + mi.num_u >= kGroupLanes) return t;
-    const int cap = h->tail_cap_env >= 0 ? h->tail_cap_env : (hess == MMPC_HESSIAN_EXACT ? 5 : 4);
+    const int cap = h->tail_cap_env >= 0 ? h->tail_cap_env : 4;
     if (cap <= 0 || cap >= p.max_iter) return t;
     const size_t inst = static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, h->nq, mi.num_shooting_nodes, false,
                                                               false, false)) * sizeof(double);
@@ -774,7 +777,9 @@ TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded, int
     t.cap = cap;
     t.gpw = gpw;
     t.lds = gpw * inst;
-    t.slots = std::min(kTailMaxSlots, per_cu * h->cu_count * gpw);
+    // up to four rounds of resume workgroups (slots nobody claimed exit at once, so spare slots cost nothing)
+    const int rounds = h->tail_rounds_env > 0 ? h->tail_rounds_env : 4;
+    t.slots = static_cast<int>(std::min<int64_t>({p.B, kTailMaxSlots, (int64_t)rounds * per_cu * h->cu_count * gpw}));
     return t;
 }
 
@@ -907,7 +912,7 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
             MMPC_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
             h->cu_count = n;
         }
-        const TailPlan tp = tail_plan(h, p, bounded, hess);
+        const TailPlan tp = tail_plan(h, p, bounded);
         SolveParams pl = p;
         if (tp.cap > 0) {   // the lane kernel hands instances still unconverged at iteration cap to a 16-lane launch
             char* const tb = reinterpret_cast<char*>(lw.ws) + solver_workspace_bytes(h, B);
@@ -1020,6 +1025,11 @@ int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_han
         char* end = nullptr;
         const long v = std::strtol(e, &end, 10);
         if (end != e && v >= 0 && v < 1000) h->tail_cap_env = static_cast<int>(v);
+    }
+    if (const char* e = std::getenv("MMPC_TAIL_ROUNDS")) {
+        char* end = nullptr;
+        const long v = std::strtol(e, &end, 10);
+        if (end != e && v > 0 && v < 1000) h->tail_rounds_env = static_cast<int>(v);
     }
     *out = h;
     g_last_error.clear();

@@ -3,8 +3,8 @@ test of iteration `cap` stop in the lane kernel and continue in a 16-lane resume
 iteration count and l1-merit weight.  Same algorithm in both kernels, so the results match the oracle as every
 same-algorithm comparison does (tests/test_gpu_parity.py _compare: V* within 1e-10 where the iteration counts agree,
 >= 99 % of the instances) and match a solve without hand-over to roundoff.  MMPC_TAIL_CAP (read at handle creation)
-forces the cap; 2 hands over most cfg#3 instances, and B = 2048 exceeds the resume launch's 768 slots, so the
-overflow path (instances that keep iterating in the lane kernel) runs too."""
+forces the cap; 2 hands over most cfg#3 instances, and B = 4096 exceeds the resume launch's slots (3072 on 256 CUs),
+so the overflow path (instances that keep iterating in the lane kernel) runs too."""
 import numpy as np
 import pytest
 
@@ -24,7 +24,7 @@ def _solve(mmpc_mod, tmp_path, monkeypatch, cap, B, N=50, seed=20250213, **kw):
     return s
 
 
-@pytest.mark.parametrize("cap,B,hess", [(2, 2048, 1), (3, 640, 1), (4, 512, 2)])
+@pytest.mark.parametrize("cap,B,hess", [(2, 4096, 1), (3, 640, 1), (4, 512, 2)])
 def test_tail_handover_vs_oracle(cap, B, hess, mmpc_mod, oracle, tmp_path, monkeypatch):
     N = 50
     x0, up, tr = oracle.synth(20250213, 0, B, N, H, model=oracle.EXO)
@@ -62,3 +62,19 @@ def test_tail_handover_device_api_and_u0(mmpc_mod, oracle, tmp_path, monkeypatch
     o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, model=oracle.EXO, kkt=oracle.KKT_RICCATI, init_states=2)
     _compare(dict(V=Vh, status=st.cpu().numpy(), iters=it.cpu().numpy()), o)
     hb.close()
+
+
+def test_tail_handover_fp32_factor_escalates_to_fp64(mmpc_mod, oracle, tmp_path, monkeypatch):
+    """cfg#5 (fp32 Riccati factor): the handed-over tail continues with the fp64 factor from the same iterate, so
+    the stop test (fp64 residuals, unchanged) holds on every instance and V* is the fp64 solution to the stop test's
+    accuracy (1e-6 relative, as tests/test_gpu_riccati.py's fp32 tests)"""
+    B, N = 768, 50
+    x0, up, tr = oracle.synth(20250213, 3, B, N, H, model=oracle.EXO)
+    r = _solve(mmpc_mod, tmp_path, monkeypatch, 2, B, factor_fp32=1).solve_batch_host(x0, up, tr, W_EXO)
+    o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, model=oracle.EXO, kkt=oracle.KKT_RICCATI, init_states=2)
+    assert (r["status"] == 0).all(), np.bincount(r["status"])
+    assert (r["kkt"] <= 1e-8).all()
+    assert (r["iters"] > 2).sum() > B // 2
+    assert _rel(r["V"], o["V"]).max() <= 1e-6
+    off = _solve(mmpc_mod, tmp_path, monkeypatch, 0, B, factor_fp32=1).solve_batch_host(x0, up, tr, W_EXO)
+    assert _rel(r["V"], off["V"]).max() <= 1e-6
