@@ -683,7 +683,8 @@ def model_flops_per_iteration(mmpc, cfg, ksolver, N, hess):
 
 
 def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_ms, hess):
-    """FP64-VALU roofline of the solve kernel (the only kernel of a step besides a memset and the result pack).
+    """FP64-VALU roofline of the solve kernel (the only kernel of a step besides a memset and the result pack; a
+    lane-kernel solve adds the 16-lane resume launch of its iteration tail, DESIGN.md 4b, inside the same bracket).
 
     achieved = the kernel's OWN algorithmic flop count (mmpc.*_flops_per_iteration: structure-exploiting, no
     flop on structural zeros, model evaluations excluded) x the SQP iterations its instances took / the mean
@@ -730,6 +731,8 @@ def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_m
             "lib_sha256": sha,
             "pmc_status": pmc_status,
             "kernel": kname,
+            "bracket": ("the lane kernel + the 16-lane resume launch of its iteration tail (DESIGN.md 4b): all of a "
+                        "solve's iterations" if ksolver == 2 else "the solve kernel"),
             "flops_per_iter_kernel_own_count": fl["total"],
             "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N, nx, nu),
             "survey_8d_equivalent_tflops": survey,
