@@ -732,7 +732,8 @@ def roofline(args, name, cfg, mmpc, solver, ksolver, N, nx, nu, B, iters, kern_m
             "pmc_status": pmc_status,
             "kernel": kname,
             "bracket": ("the lane kernel + the 16-lane resume launch of its iteration tail (DESIGN.md 4b): all of a "
-                        "solve's iterations" if ksolver == 2 else "the solve kernel"),
+                        "solve's iterations" if ksolver == 2 and args.u_bound is None and args.x_bound is None
+                        else "the solve kernel"),
             "flops_per_iter_kernel_own_count": fl["total"],
             "flops_per_iter_survey_8d": mmpc.survey_flops_per_iteration(N, nx, nu),
             "survey_8d_equivalent_tflops": survey,
