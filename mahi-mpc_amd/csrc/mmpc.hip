@@ -80,6 +80,7 @@ struct mmpc_handle {
     // iteration-tail hand-over: cap override from MMPC_TAIL_CAP at creation (-1: the default policy),
     // compute units of the device (slots of the resume launch)
     int tail_cap_env = -1;
+    int tail_wave_env = -1;    // MMPC_TAIL_WAVE: hand over when at most this many lanes of a wave are left (-1: 8)
     int tail_rounds_env = -1;   // MMPC_TAIL_ROUNDS: rounds of resume workgroups (-1: 4)
     int cu_count = 0;
     // state bounds of x_1..x_N (JSON x_min/x_max, or mmpc_set_state_bounds); copied into each launch's arguments
@@ -759,7 +760,7 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
 // workgroups (groups per workgroup gpw with <= 64 KB of LDS, up to 4 one-wave workgroups per CU per round),
 // MMPC_TAIL_ROUNDS overrides.
 struct TailPlan {
-    int cap = 0, slots = 0, gpw = 1;
+    int cap = 0, wave_max = 0, slots = 0, gpw = 1;
     size_t lds = 0;
 };
 TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded) {
@@ -775,6 +776,7 @@ TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded) {
     const int gpw = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kGroupsPerWave, (64 * 1024) / inst)));
     const int per_cu = static_cast<int>(std::min<size_t>(4, (160 * 1024) / (gpw * inst)));
     t.cap = cap;
+    t.wave_max = h->tail_wave_env >= 0 ? h->tail_wave_env : 8;
     t.gpw = gpw;
     t.lds = gpw * inst;
     // up to four rounds of resume workgroups (slots nobody claimed exit at once, so spare slots cost nothing)
@@ -818,6 +820,7 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.init_hold = h->opts.init_states == MMPC_INIT_HOLD_X0;
     p.init_zero = h->opts.init_states == MMPC_INIT_ZERO;
     p.tail_cap = 0;
+    p.tail_wave_max = 0;
     p.tail_slots = 0;
     p.tail_count = p.tail_idx = p.tail_it = nullptr;
     p.tail_mu = nullptr;
@@ -917,6 +920,7 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         if (tp.cap > 0) {   // the lane kernel hands instances still unconverged at iteration cap to a 16-lane launch
             char* const tb = reinterpret_cast<char*>(lw.ws) + solver_workspace_bytes(h, B);
             pl.tail_cap = tp.cap;
+            pl.tail_wave_max = tp.wave_max;
             pl.tail_slots = tp.slots;
             pl.tail_count = reinterpret_cast<int32_t*>(tb);
             pl.tail_idx = reinterpret_cast<int32_t*>(tb + 256);
@@ -1025,6 +1029,11 @@ int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_han
         char* end = nullptr;
         const long v = std::strtol(e, &end, 10);
         if (end != e && v >= 0 && v < 1000) h->tail_cap_env = static_cast<int>(v);
+    }
+    if (const char* e = std::getenv("MMPC_TAIL_WAVE")) {
+        char* end = nullptr;
+        const long v = std::strtol(e, &end, 10);
+        if (end != e && v >= 0 && v <= 64) h->tail_wave_env = static_cast<int>(v);
     }
     if (const char* e = std::getenv("MMPC_TAIL_ROUNDS")) {
         char* end = nullptr;

@@ -954,8 +954,13 @@ sqp_lane_kernel(SolveParams p,
                     break;
                 }
                 // tail hand-over (unbounded solves): the instance continues in a 16-lane resume launch from this
-                // iterate, iteration count and merit weight -- the wave no longer waits for it
-                if (!BOUNDED && !XB && p.tail_cap > 0 && it == p.tail_cap) {
+                // iterate, iteration count and merit weight -- the wave no longer waits for it.  At iteration
+                // tail_cap (and later, after an overflow), or earlier (from iteration 2) once at most tail_wave_max
+                // lanes of the wave are still iterating: the active lanes here are exactly the unconverged ones
+                bool hand = !BOUNDED && !XB && p.tail_cap > 0 && it >= p.tail_cap;
+                if (!BOUNDED && !XB && p.tail_cap > 0 && !hand && it >= 2 && p.tail_wave_max > 0)
+                    hand = __popcll(__ballot(1)) <= p.tail_wave_max;
+                if (hand) {
                     const int slot = atomicAdd(p.tail_count, 1);
                     if (slot < p.tail_slots) {
                         p.tail_idx[slot] = (int32_t)inst;

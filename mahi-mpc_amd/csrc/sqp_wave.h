@@ -66,6 +66,7 @@ struct SolveParams {
     // stops with its iterate written back; a 16-lane resume launch over the list continues it from there, with the
     // same iteration count and l1-merit weight.  Instances beyond tail_slots keep iterating in the lane kernel.
     int tail_cap;          // 0: no hand-over
+    int tail_wave_max;     // also hand over at iterations >= 2 when at most this many lanes of the wave are left
     int tail_slots;        // capacity of the list
     int32_t* tail_count;   // [1] claims (may exceed tail_slots)
     int32_t* tail_idx;     // [tail_slots] instance; in a 16-lane launch, non-null = resume launch over the list

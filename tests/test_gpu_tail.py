@@ -78,3 +78,23 @@ def test_tail_handover_fp32_factor_escalates_to_fp64(mmpc_mod, oracle, tmp_path,
     assert _rel(r["V"], o["V"]).max() <= 1e-6
     off = _solve(mmpc_mod, tmp_path, monkeypatch, 0, B, factor_fp32=1).solve_batch_host(x0, up, tr, W_EXO)
     assert _rel(r["V"], off["V"]).max() <= 1e-6
+
+
+def test_tail_handover_wave_rule_loose_tolerance(mmpc_mod, oracle, tmp_path, monkeypatch):
+    """the wave rule (hand over from iteration 2 once at most MMPC_TAIL_WAVE lanes of a wave are left) at the
+    reference's IPOPT tolerance (tol 1e-5, defects 1e-7), where the stragglers need the 4th iteration: same iterates
+    as without hand-over, against the oracle with the same tolerances"""
+    B, N, tg, td = 1024, 50, 1e-5, 1e-7
+    x0, up, tr = oracle.synth(20250213, 5, B, N, H, model=oracle.EXO)
+    monkeypatch.setenv("MMPC_TAIL_WAVE", "16")
+    s = _solve(mmpc_mod, tmp_path, monkeypatch, 9, B, tol_grad=tg, tol_defect=td)
+    monkeypatch.delenv("MMPC_TAIL_WAVE")
+    r = s.solve_batch_host(x0, up, tr, W_EXO)
+    o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, model=oracle.EXO, kkt=oracle.KKT_RICCATI, init_states=2,
+                           tol_grad=tg, tol_defect=td)
+    assert (r["status"] == 0).all()
+    _compare(r, o)
+    off = _solve(mmpc_mod, tmp_path, monkeypatch, 0, B, tol_grad=tg, tol_defect=td).solve_batch_host(x0, up, tr, W_EXO)
+    assert (off["iters"] == r["iters"]).mean() >= 0.99
+    same = off["iters"] == r["iters"]
+    assert _rel(r["V"][same], off["V"][same]).max() <= 1e-10

@@ -12,7 +12,7 @@ run() {  # tag kernel-substring key batch horizon bench-args
   local tag=$1 kern=$2 key=$3 batch=$4 hor=$5 bargs=$6
   local tj="$OUT/traffic_latest.json"
   OUT="$OUT/$tag" KERNEL="$kern" BENCH_ARGS="$bargs" \
-    SUMMARY_ARGS="--traffic-json $tj --key $key --batch $batch --horizon $hor --source ${PMC_LABEL_DIR:-profiles/r05/final/pmc}/${tag}_pmc_summary.json" \
+    SUMMARY_ARGS="--traffic-json $tj --key $key --batch $batch --horizon $hor --source ${PMC_LABEL_DIR:-profiles/r05/final2/pmc}/${tag}_pmc_summary.json" \
     bash tools/pmc.sh > "$OUT/$tag.log" 2>&1 || { echo "pmc $tag failed"; tail -20 "$OUT/$tag.log"; return 1; }
   python3 -c "import json; d=json.load(open('$OUT/$tag/pmc_summary.json')); print('$tag', d.get('kernel_ms_trace_pass'), d.get('hbm_bytes_per_launch'), d.get('fp64_valu_frac_of_peak'), d.get('lib_sha256')[:12])"
 }
