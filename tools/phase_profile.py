@@ -42,7 +42,8 @@ if a.x_bound is not None:
     s.set_state_bounds([-np.inf] * (nx // 2) + [-a.x_bound] * (nx // 2), [np.inf] * (nx // 2) + [a.x_bound] * (nx // 2))
 NAMES_GROUP = ["load", "A:evals(parallel)", "B:d+adjoint(+riccati if not DIST)", "riccati(DIST)+mu",
                "C:step(serial)+dJ", "D:line_search", "after_loop", "writeback", "update(loop top)", "check"]
-if a.kkt == 3:
+ksolver = s.kkt_solver_for(B)   # the AUTO choice resolved
+if ksolver == 3:
     NAMES = NAMES_GROUP
 elif exo or a.kkt == 2 or N * nu > 64:
     NAMES = NAMES_LANE
