@@ -101,7 +101,12 @@ enum mmpc_kkt_solver {
                                B <= 2560, RICCATI_GROUP up to B*N = 1e6, else RICCATI; exo -- RICCATI_GROUP
                                for B <= 4096 when two workgroups fit a CU's LDS, else RICCATI */
     MMPC_KKT_CONDENSED = 1, /* one wavefront per instance, condensed Hessian row per lane (N*nu <= 64) */
-    MMPC_KKT_RICCATI = 2,   /* one lane per instance, Riccati recursion, any N (needs a workspace) */
+    MMPC_KKT_RICCATI = 2,   /* one lane per instance, Riccati recursion, any N (needs a workspace).  Unbounded
+                               nonlinear solves of models with nx+nu < 16 hand instances still unconverged after
+                               iteration 4 (or once at most 8 lanes of their wave are left) to a 16-lane resume
+                               launch on the same stream that continues the same iterates; with
+                               factor_fp32 that tail runs the fp64 factor.  Env MMPC_TAIL_CAP / MMPC_TAIL_WAVE /
+                               MMPC_TAIL_ROUNDS, read at mmpc_create (0 = off), override the policy */
     MMPC_KKT_RICCATI_GROUP = 3 /* 16 lanes per instance: stage-parallel model evaluations and line search,
                                   serial Riccati sweeps from LDS (stage data of 4 instances <= 160 KB LDS) */
 };
@@ -181,7 +186,8 @@ int mmpc_set_state_bounds(mmpc_handle* h, const double* x_lb, const double* x_ub
 int mmpc_get_state_bounds(const mmpc_handle* h, double* x_lb, double* x_ub);
 
 /* Pre-allocate the Riccati solvers' device workspace for batches up to B (so that later
- * stream-ordered solves allocate nothing; the workspace grows on demand otherwise).  *bytes (may be NULL) receives the workspace size. */
+ * stream-ordered solves allocate nothing; the workspace grows on demand otherwise; it includes the iteration-tail
+ * hand-over list).  *bytes (may be NULL) receives the workspace size. */
 int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes);
 
 /* The KKT solver (enum mmpc_kkt_solver) a solve of B instances runs under the handle's options:
