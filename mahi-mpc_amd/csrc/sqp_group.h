@@ -22,6 +22,12 @@
 
 namespace mmpc {
 
+#ifndef MMPC_GROUP_BOUNDED_PAIRS
+#define MMPC_GROUP_BOUNDED_PAIRS 0
+#endif
+#ifndef MMPC_GROUP_XB_PAIRS
+#define MMPC_GROUP_XB_PAIRS 1
+#endif
 constexpr int kGroupLanes = 16;
 constexpr int kGroupsPerWave = 4;
 
@@ -1334,9 +1340,14 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 if constexpr (BOUNDED) pv2 += pexr;
                 pvr = pv2;
             };
-            // inner stages N-1 .. 1 by unconditional pairs (an odd count peels stage N-1 in front), as the step sweep
+            // inner stages N-1 .. 1 by unconditional pairs (an odd count peels stage N-1 in front), as the step sweep;
+            // the control-bounded sweep one stage per trip (its hold logic and relaxation rows fill the registers: two
+            // stages in flight spilled to scratch inside the loop)
             using F_ = std::false_type;
-            if ((N - 1) & 1) {
+            if constexpr ((BOUNDED && !MMPC_GROUP_BOUNDED_PAIRS) || (XB && !MMPC_GROUP_XB_PAIRS)) {
+                for (int k = N - 1; k >= 1; --k) stage(k, F_{}, w0);
+                stage(0, std::true_type{}, w0);
+            } else if ((N - 1) & 1) {
                 stage(N - 1, F_{}, w0);
                 for (int k = N - 2; k >= 2; k -= 2) {
                     stage(k, F_{}, w0);
