@@ -44,6 +44,12 @@
 #ifndef MMPC_LANE_WPE32
 #define MMPC_LANE_WPE32 1
 #endif
+#ifndef MMPC_LANE_XB_EARLY
+#define MMPC_LANE_XB_EARLY 1
+#endif
+#ifndef MMPC_LANE_XB_EARLY_STEP
+#define MMPC_LANE_XB_EARLY_STEP MMPC_LANE_XB_EARLY
+#endif
 
 namespace mmpc {
 
@@ -449,6 +455,16 @@ sqp_lane_kernel(SolveParams p,
                     xn[r] = SK(1, FX, r);
                     rk[r] = SK(0, SF::R, r);
                 }
+                // XB: this stage's duals, loaded before the model evaluation (their latency hides behind it)
+                constexpr int XF = (XB && MMPC_LANE_XB_EARLY) ? NY : 1;
+                double zlf[XF], zuf[XF];
+                if constexpr (XB && MMPC_LANE_XB_EARLY) {
+#pragma unroll
+                    for (int j = 0; j < NY; ++j) {
+                        zlf[j] = SK(0, SF::ZL, j);
+                        zuf[j] = SK(0, SF::ZU, j);
+                    }
+                }
                 double dn[NX];   // A_k d_k
                 if (JVP && !lin) {
                     double zu[NU], jv[NA];
@@ -484,8 +500,15 @@ sqp_lane_kernel(SolveParams p,
 #pragma unroll
                     for (int j = 0; j < NY; ++j) {
                         double sg, bb, zg;
-                        ip_terms(j < NX ? xk[j] : u[j - NX], yl[j], yu[j], SK(0, SF::ZL, j), SK(0, SF::ZU, j), mub, sg,
-                                 bb, zg, cmpl0, cmplmu, lsum);
+                        double zl, zu;
+                        if constexpr (MMPC_LANE_XB_EARLY) {
+                            zl = zlf[j];
+                            zu = zuf[j];
+                        } else {
+                            zl = SK(0, SF::ZL, j);
+                            zu = SK(0, SF::ZU, j);
+                        }
+                        ip_terms(j < NX ? xk[j] : u[j - NX], yl[j], yu[j], zl, zu, mub, sg, bb, zg, cmpl0, cmplmu, lsum);
                         SK(0, SF::SG, j) = sg;
                         SK(0, SF::BB, j) = bb;
                         SK(0, SF::ZG, j) = zg;
@@ -580,6 +603,33 @@ sqp_lane_kernel(SolveParams p,
                     }
 #pragma unroll
                     for (int c = 0; c < NU; ++c) upf[c] = um[c];
+                    // XB: the barrier pieces this stage adds (u part of stage k, x part of stage k-1), loaded before the
+                    // model evaluation so that their latency hides behind it (read at their uses they stalled the sweep)
+                    constexpr int XE = (XB && MMPC_LANE_XB_EARLY) ? 1 : 0;
+                    double zgu[XE ? NU : 1], sgu[XE ? NU : 1], bbu[XE ? NU : 1], zgx[XE ? NX : 1], sgx[XE ? NX : 1],
+                        bbx[XE ? NX : 1];
+                    if constexpr (XE) {
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) {
+                            zgu[c] = SK(0, SF::ZG, NX + c);
+                            sgu[c] = SK(0, SF::SG, NX + c);
+                            bbu[c] = SK(0, SF::BB, NX + c);
+                        }
+                        if (k >= 1) {
+#pragma unroll
+                            for (int r = 0; r < NX; ++r) {
+                                zgx[r] = SK(-1, SF::ZG, r);
+                                sgx[r] = SK(-1, SF::SG, r);
+                                bbx[r] = SK(-1, SF::BB, r);
+                            }
+                        }
+                    }
+                    auto xb_zgu = [&](int c) { if constexpr (XE) return zgu[c]; else return (double)SK(0, SF::ZG, NX + c); };
+                    auto xb_sgu = [&](int c) { if constexpr (XE) return sgu[c]; else return (double)SK(0, SF::SG, NX + c); };
+                    auto xb_bbu = [&](int c) { if constexpr (XE) return bbu[c]; else return (double)SK(0, SF::BB, NX + c); };
+                    auto xb_zgx = [&](int r) { if constexpr (XE) return zgx[r]; else return (double)SK(-1, SF::ZG, r); };
+                    auto xb_sgx = [&](int r) { if constexpr (XE) return sgx[r]; else return (double)SK(-1, SF::SG, r); };
+                    auto xb_bbx = [&](int r) { if constexpr (XE) return bbx[r]; else return (double)SK(-1, SF::BB, r); };
                     STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
                     // exact Hessian: W_k at (x_k, u_k) with lam_{k+1} (lam holds it until the adjoint step below)
                     constexpr int KZ = NX + NU;
@@ -603,7 +653,7 @@ sqp_lane_kernel(SolveParams p,
                         for (int s = 0; s < NA; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
                         g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
                         if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
-                        if (XB) g += SK(0, SF::ZG, NX + c);  // reduced Lagrangian gradient
+                        if (XB) g += xb_zgu(c);  // reduced Lagrangian gradient
                         if (!BOUNDED) {
                             gmax = fmax(gmax, fabs(2.0 * g));
                         } else {  // projected gradient; hold rule (pass 0) or the holds of the previous solve
@@ -627,7 +677,7 @@ sqp_lane_kernel(SolveParams p,
 #pragma unroll
                         for (int r = 0; r < NX; ++r) {
                             lam[r] = fma(Q[r], dk[r] + x[r] - rkm[r], ln[r]);
-                            if (XB) lam[r] += SK(-1, SF::ZG, r);
+                            if (XB) lam[r] += xb_zgx(r);
                             lmax = fmax(lmax, fabs(lam[r]));
                         }
                     }
@@ -673,12 +723,12 @@ sqp_lane_kernel(SolveParams p,
                             for (int s = 0; s < NA; ++s)
                                 t = fma(fu[s * NU + a], G[NQ + s][b], fma(PS(NQ + s, NX + a), fu[s * NU + b], t));
                             if (a == b) t += (FT)(R[a] + Rm[a]);
-                            if (XB && a == b) t += (FT)SK(0, SF::SG, NX + a);
+                            if (XB && a == b) t += (FT)xb_sgu(a);
                             if constexpr (EXACT) t += Wk[(NX + a) * KZ + NX + b];
                             Hww[a][b] = t;
                         }
                         double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], pv[NX + a]));
-                        if (XB) t += SK(0, SF::BB, NX + a);
+                        if (XB) t += xb_bbu(a);
 #pragma unroll
                         for (int s = 0; s < NA; ++s) t = fma(hFu[s * NU + a], mv[NQ + s], t);
 #pragma unroll
@@ -754,7 +804,7 @@ sqp_lane_kernel(SolveParams p,
 #pragma unroll
                         for (int q = 0; q < NX; ++q) {
                             pn[q] = fma(Q[q], x[q] - rkm[q], t[q]);
-                            if (XB) pn[q] += SK(-1, SF::BB, q);
+                            if (XB) pn[q] += xb_bbx(q);
                         }
 #pragma unroll
                         for (int c = 0; c < NU; ++c) pn[NX + c] = -R[c] * (u[c] - um[c]);
@@ -851,7 +901,7 @@ sqp_lane_kernel(SolveParams p,
                             for (int b = 0; b < NX; ++b) WB(s2, b) = wrow[b];
                         }
                         auto out = [&](int a, int b, FT v) {
-                            v += (FT)((a == b) ? Q[a] + (XB ? SK(-1, SF::SG, a) : 0.0) : 0.0);
+                            v += (FT)((a == b) ? Q[a] + (XB ? xb_sgx(a) : 0.0) : 0.0);
                             if constexpr (EXACT) v += Wk[a * KZ + b];   // + W_xx
 #pragma unroll
                             for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
@@ -898,7 +948,7 @@ sqp_lane_kernel(SolveParams p,
                         at_mul<NQ, NA, FT>(hf, fq, fqd, wcol, col);
 #pragma unroll
                         for (int a = 0; a <= b; ++a) {
-                            FT v = col[a] + (FT)((a == b) ? Q[a] + (XB ? SK(-1, SF::SG, a) : 0.0) : 0.0);
+                            FT v = col[a] + (FT)((a == b) ? Q[a] + (XB ? xb_sgx(a) : 0.0) : 0.0);
                             if constexpr (EXACT) v += Wk[a * KZ + b];   // + W_xx
 #pragma unroll
                             for (int q = 0; q < NU; ++q) v = fma(-Y[q][a], Y[q][b], v);
@@ -1035,6 +1085,18 @@ sqp_lane_kernel(SolveParams p,
                     for (int c = 0; c < NU; ++c) {
                         u[c] = upf[c];
                         upf[c] = SK(1, FU, c);  // stage N's U slot exists (unused) when k = N-1
+                    }
+                    // XB: the duals and barrier gradient of this stage for the fraction to the boundary, loaded before
+                    // the model evaluation (read at their use, at the end of the stage, they stalled the sweep)
+                    constexpr int XS = (XB && MMPC_LANE_XB_EARLY_STEP) ? NY : 1;
+                    double zls[XS], zus[XS], bbs[XS];
+                    if constexpr (XB && MMPC_LANE_XB_EARLY_STEP) {
+#pragma unroll
+                        for (int j = 0; j < NY; ++j) {
+                            zls[j] = SK(0, SF::ZL, j);
+                            zus[j] = SK(0, SF::ZU, j);
+                            bbs[j] = SK(0, SF::BB, j);
+                        }
                     }
                     double du[NU];
                     const gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
@@ -1176,10 +1238,20 @@ sqp_lane_kernel(SolveParams p,
                     }
                     if constexpr (XB) {  // fraction to the boundary of (x_{k+1} | u_k), barrier directional derivative
 #pragma unroll
-                        for (int j = 0; j < NY; ++j)
-                            ip_step_limits(j < NX ? xpf[j] : u[j - NX], j < NX ? dx[j] : du[j - NX], yl[j], yu[j],
-                                           SK(0, SF::ZL, j), SK(0, SF::ZU, j), mub, kIpTau, SK(0, SF::BB, j), amax,
-                                           az, dbar);
+                        for (int j = 0; j < NY; ++j) {
+                            double zl, zu, bb;
+                            if constexpr (MMPC_LANE_XB_EARLY_STEP) {
+                                zl = zls[j];
+                                zu = zus[j];
+                                bb = bbs[j];
+                            } else {
+                                zl = SK(0, SF::ZL, j);
+                                zu = SK(0, SF::ZU, j);
+                                bb = SK(0, SF::BB, j);
+                            }
+                            ip_step_limits(j < NX ? xpf[j] : u[j - NX], j < NX ? dx[j] : du[j - NX], yl[j], yu[j], zl,
+                                           zu, mub, kIpTau, bb, amax, az, dbar);
+                        }
                     }
                 }
             }
