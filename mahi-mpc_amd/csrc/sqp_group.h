@@ -1033,6 +1033,20 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     um[c] = LAST ? up[c] : sU[(k - 1) * NU + c];
                 }
                 load_acol(k, acol);
+                // XB: the barrier pieces of this stage (u_k) and of x_k (stage k-1), loaded with the stage operands:
+                // read at their uses, deep in the stage, their HBM latency was exposed
+                double xsgu[XB ? NU : 1], xbbu[XB ? NU : 1], xsgx = 0.0, xbbx = 0.0;
+                if constexpr (XB) {
+#pragma unroll
+                    for (int a = 0; a < NU; ++a) {
+                        xsgu[a] = sSg[k * NY + NX + a];
+                        xbbu[a] = sBb[k * NY + NX + a];
+                    }
+                    if constexpr (!LAST) {
+                        xsgx = sSg[(k - 1) * NY + rx];
+                        xbbx = sBb[(k - 1) * NY + rx];
+                    }
+                }
                 double exr = 0.0, duu = 0.0;
                 if constexpr (!LAST) {
                     const double xk = sX[k * NX + rx], trm = tr[(k - 1) * NX + rx];
@@ -1076,7 +1090,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         if (a == b) t += R[a] + Rm[a];
                         if constexpr (EXACT && !CAFF) t += wu[a * NU + b];
                         if constexpr (XB) {
-                            if (a == b) t += sSg[k * NY + NX + a];   // barrier Sigma of u_k
+                            if (a == b) t += xsgu[a];   // barrier Sigma of u_k
                         }
                         Hww[a][b] = t;
                         Hww[b][a] = t;
@@ -1084,7 +1098,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                     double t = fma(R[a], u[a] - um[a], fma(Rm[a], u[a], mvb[NX + a]));
 #pragma unroll
                     for (int s2 = 0; s2 < NA; ++s2) t = fma(hFu[s2 * NU + a], mvb[NQ + s2], t);
-                    if constexpr (XB) t += sBb[k * NY + NX + a];   // barrier gradient b of u_k
+                    if constexpr (XB) t += xbbu[a];   // barrier gradient b of u_k
                     hw[a] = t;
                 }
                 // column r of Y = [H_wx | -R | .]: x-lanes (A^T T)[r], u-lanes -R e_{r-NX}
@@ -1295,8 +1309,8 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 double pn = fma(-Rr, duu, lxm * fma(Qr, exr, colA(mv, acol, mvb)));
                 double sgk = 0.0;   // XB: barrier Sigma and b of x_k (stage k-1's y)
                 if constexpr (XB) {
-                    sgk = sSg[(k - 1) * NY + rx];
-                    pn = fma(lxm, sBb[(k - 1) * NY + rx], pn);
+                    sgk = xsgx;
+                    pn = fma(lxm, xbbx, pn);
                 }
                 if constexpr (XB) {   // P~_k = blkdiag(A^T P_xx A + Q + Sigma, R) - Ytil^T Ytil, p~_k = pn - Ytil^T htil
                     double Yb[NU][NS];
