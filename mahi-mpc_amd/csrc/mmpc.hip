@@ -738,9 +738,10 @@ int ensure_workspace_bytes(mmpc_handle* h, size_t bytes, double** out) {
     *out = h->ws;
     return MMPC_OK;
 }
-// iteration-tail hand-over list after the solver workspace: [count | pad][idx: slots x i32][it: slots x i32][mu]
+// iteration-tail hand-over list after the solver workspace: [count | pad][idx: slots x i32][it: slots x i32][mu][mub]
+// (a state-bounded solve's resume workspace follows it: its duals stay in the lane launch's workspace)
 constexpr int kTailMaxSlots = 65536;
-constexpr size_t kTailBytes = 256 + static_cast<size_t>(kTailMaxSlots) * 16;
+constexpr size_t kTailBytes = 256 + static_cast<size_t>(kTailMaxSlots) * 24;
 size_t solver_workspace_bytes(const mmpc_handle* h, int64_t B) {
     return (std::max(workspace_bytes(h->info, h->nq, B), group_workspace_bytes(h->info, B)) + 255) / 256 * 256;
 }
@@ -759,30 +760,53 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
 // Hessian; 3 hands over too many: cfg#3 12.8 ms), MMPC_TAIL_CAP overrides (0 = off). slots: four rounds of resume
 // workgroups (groups per workgroup gpw with <= 64 KB of LDS, up to 4 one-wave workgroups per CU per round),
 // MMPC_TAIL_ROUNDS overrides.
+// State-bounded (interior-point) solves hand over by the wave rule alone (their counts spread over 10-21 iterations
+// at the exo's cfg#3 size: no common cap), the duals read from the lane launch's workspace by the resume launch,
+// whose own workspace then lies after the hand-over list (xb_ws_bytes).
 struct TailPlan {
     int cap = 0, wave_max = 0, slots = 0, gpw = 1;
-    size_t lds = 0;
+    size_t lds = 0, xb_ws_bytes = 0;
 };
-TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded) {
+TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded, int cu) {
     TailPlan t;
     const mmpc_model_info& mi = h->info;
-    if (bounded || p.x_bounded || mi.is_linear || p.trace || h->cu_count <= 0) return t;
+    const bool xb = p.x_bounded != 0;
+    if ((bounded && !xb) || mi.is_linear || p.trace || cu <= 0) return t;
     if (mi.num_x + mi.num_u >= kGroupLanes) return t;
-    const int cap = h->tail_cap_env >= 0 ? h->tail_cap_env : 4;
-    if (cap <= 0 || cap >= p.max_iter) return t;
+    constexpr int kNoCap = 1 << 20;
+    const int cap = h->tail_cap_env >= 0 ? h->tail_cap_env : (xb ? kNoCap : 4);
+    if (cap <= 0 || (cap >= p.max_iter && !xb)) return t;
+    // wave rule threshold: 8 lanes (Gauss-Newton / exact: only the thin tails of loose tolerances use it), 4 for
+    // interior-point solves, whose handed-over instances need several more iterations (exo |qdot| <= 1.5 at cfg#3
+    // size: 65.3 ms without, 62.2 / 61.0 / 61.0 / 60.5 / 67.6 ms at 1 / 2 / 3 / 4 / 6, profiles/r05/xbwave)
+    const int wave_max = h->tail_wave_env >= 0 ? h->tail_wave_env : (xb ? 4 : 8);
+    if (xb && cap >= p.max_iter && wave_max <= 0) return t;
     const size_t inst = static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, h->nq, mi.num_shooting_nodes, false,
-                                                              false, false)) * sizeof(double);
+                                                              false, xb)) * sizeof(double);
     if (inst > 64 * 1024) return t;
     const int gpw = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kGroupsPerWave, (64 * 1024) / inst)));
     const int per_cu = static_cast<int>(std::min<size_t>(4, (160 * 1024) / (gpw * inst)));
     t.cap = cap;
-    t.wave_max = h->tail_wave_env >= 0 ? h->tail_wave_env : 8;
+    t.wave_max = wave_max;
     t.gpw = gpw;
     t.lds = gpw * inst;
     // up to four rounds of resume workgroups (slots nobody claimed exit at once, so spare slots cost nothing)
     const int rounds = h->tail_rounds_env > 0 ? h->tail_rounds_env : 4;
-    t.slots = static_cast<int>(std::min<int64_t>({p.B, kTailMaxSlots, (int64_t)rounds * per_cu * h->cu_count * gpw}));
+    t.slots = static_cast<int>(std::min<int64_t>({p.B, kTailMaxSlots, (int64_t)rounds * per_cu * cu * gpw}));
+    if (xb)
+        t.xb_ws_bytes = static_cast<size_t>(group_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes, false, true)) *
+                        static_cast<size_t>(t.slots) * sizeof(double);
     return t;
+}
+// the device's compute units (the resume launch's slots scale with them), queried once per handle
+int query_cu_count(mmpc_handle* h) {
+    if (h->cu_count == 0) {
+        int dev = 0, n = 0;
+        MMPC_HIP(hipGetDevice(&dev));
+        MMPC_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+        h->cu_count = n;
+    }
+    return MMPC_OK;
 }
 
 int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,
@@ -823,7 +847,10 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.tail_wave_max = 0;
     p.tail_slots = 0;
     p.tail_count = p.tail_idx = p.tail_it = nullptr;
-    p.tail_mu = nullptr;
+    p.tail_mu = p.tail_mub = nullptr;
+    p.tail_lws = nullptr;
+    p.tail_lws_block = 0;
+    p.tail_lws_ss = p.tail_lws_zl = 0;
     p.gpw = kGroupsPerWave;
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
     // points pass NULL for bounds that are all infinite
@@ -905,17 +932,13 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         return fail(MMPC_ERR_UNSUPPORTED, "condensed solver needs the built-in 2-link arm");
 #endif
     } else {
+        int rc = query_cu_count(h);
+        if (rc) return rc;
+        const TailPlan tp = tail_plan(h, p, bounded, h->cu_count);
         LaneWork lw;
-        int rc = ensure_workspace(h, B, &lw);
+        rc = ensure_workspace_bytes(h, solver_workspace_bytes(h, B) + kTailBytes + tp.xb_ws_bytes, &lw.ws);
         if (rc) return rc;
         dim3 grid(grid1d(B, 64)), block(64);
-        if (h->cu_count == 0) {   // the resume launch's slots scale with the compute units
-            int dev = 0, n = 0;
-            MMPC_HIP(hipGetDevice(&dev));
-            MMPC_HIP(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
-            h->cu_count = n;
-        }
-        const TailPlan tp = tail_plan(h, p, bounded);
         SolveParams pl = p;
         if (tp.cap > 0) {   // the lane kernel hands instances still unconverged at iteration cap to a 16-lane launch
             char* const tb = reinterpret_cast<char*>(lw.ws) + solver_workspace_bytes(h, B);
@@ -926,6 +949,7 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
             pl.tail_idx = reinterpret_cast<int32_t*>(tb + 256);
             pl.tail_it = pl.tail_idx + kTailMaxSlots;
             pl.tail_mu = reinterpret_cast<double*>(pl.tail_it + kTailMaxSlots);
+            pl.tail_mub = pl.tail_mu + kTailMaxSlots;
             MMPC_HIP(hipMemsetAsync(pl.tail_count, 0, sizeof(int32_t), stream));
         }
         // lane kernels: their own translation unit (lane_kernels.hip, lane_launch.h)
@@ -938,17 +962,28 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
             pr.tail_cap = 0;
             pr.gpw = tp.gpw;
             pr.init_hold = pr.init_zero = 0;   // the handed-over iterate is in V
+            const bool xb = p.x_bounded != 0;
             GroupWork gwk{lw.ws};
+            if (xb) {   // duals from the lane workspace; the resume workspace after the hand-over list
+                const int nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes;
+                pr.tail_lws = lw.ws;
+                pr.tail_lws_block = static_cast<int64_t>(lane_ws_doubles(nx, nu, h->nq, N, true)) * 64;
+                pr.tail_lws_ss = lane_stage_stride(nx, nu, true);
+                pr.tail_lws_zl = lane_zl_offset(nx, nu);
+                gwk.ws = lw.ws + (solver_workspace_bytes(h, B) + kTailBytes) / sizeof(double);
+            }
             dim3 rgrid(static_cast<unsigned>((tp.slots + tp.gpw - 1) / tp.gpw)), rblock(64);
             rc = with_model(mi.model_id, [&](auto* m) {
                 using M = std::remove_pointer_t<decltype(m)>;
                 if constexpr (M::NX + M::NU < kGroupLanes) {
                     if constexpr (std::is_same<M, TwoLinkArm>::value) {
-                        const hipError_t e = launch_group_two_link(hess == MMPC_HESSIAN_EXACT, rgrid, rblock, tp.lds,
-                                                                   stream, pr, gwk);
+                        const hipError_t e =
+                            xb ? launch_group_two_link_bounded(true, false, rgrid, rblock, tp.lds, stream, pr, gwk)
+                               : launch_group_two_link(hess == MMPC_HESSIAN_EXACT, rgrid, rblock, tp.lds, stream, pr, gwk);
                         return e == hipSuccess ? MMPC_OK : fail(MMPC_ERR_HIP, std::string("resume launch: ") +
                                                                                   hipGetErrorString(e));
                     } else {
+                        if (xb) return launch_group<M, false, true>(rgrid, rblock, tp.lds, stream, pr, gwk);
                         if constexpr (exact_capable<M>()) {
                             if (hess == MMPC_HESSIAN_EXACT)
                                 return launch_group<M, false, false, true>(rgrid, rblock, tp.lds, stream, pr, gwk);
@@ -1110,16 +1145,28 @@ int mmpc_get_state_bounds(const mmpc_handle* h, double* x_lb, double* x_ub) {
 int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes) {
     if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
     if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
-    const size_t nb = B == 0 ? 0 : solver_workspace_bytes(h, B) + kTailBytes;   // + the tail hand-over list
-    if (bytes) *bytes = nb;
+    // + the tail hand-over list (+ a state-bounded solve's resume workspace, sized by the device's CUs: 256 until
+    // a device was queried)
+    auto total = [&]() {
+        SolveParams p{};
+        p.B = B;
+        p.max_iter = h->opts.max_iter;
+        p.x_bounded = h->x_bounded;
+        p.is_linear = h->info.is_linear;
+        const int cu = h->cu_count > 0 ? h->cu_count : 256;
+        return solver_workspace_bytes(h, B) + kTailBytes + (h->x_bounded ? tail_plan(h, p, false, cu).xb_ws_bytes : 0);
+    };
+    if (bytes) *bytes = B == 0 ? 0 : total();
     if (B == 0) return MMPC_OK;
     int dev;
     int rc = resolve_device(h, &dev);
     if (rc) return rc;
     DeviceGuard g(dev);
     if (g.err) return fail(MMPC_ERR_NO_DEVICE, "cannot select device");
-    LaneWork lw;
-    return ensure_workspace(h, B, &lw);
+    if ((rc = query_cu_count(h))) return rc;
+    if (bytes) *bytes = total();
+    double* ws = nullptr;
+    return ensure_workspace_bytes(h, total(), &ws);
 }
 
 int mmpc_solve_batch(mmpc_handle* h, int64_t B, const double* x0, const double* u_prev, const double* traj,

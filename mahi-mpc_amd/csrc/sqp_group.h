@@ -286,18 +286,29 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     }
     const double* const tr = sR;
     double yl[XB ? NY : 1], yu[XB ? NY : 1];
-    double mub = kIpMu0;  // barrier parameter (f = J/2 scale)
+    double mub = (XB && resume) ? p.tail_mub[slot] : kIpMu0;  // barrier parameter (f = J/2 scale)
     if constexpr (XB) {
         load_ip_bounds<NX, NU>(p, yl, yu);
         __builtin_amdgcn_wave_barrier();
-        // y pushed into the interior, z = 1 on finite bounds (oracle solve_one_ip)
-        for (int k = gl; k < N; k += G) {
+        if (resume) {   // the handed-over duals, from the lane launch's workspace (the iterate is interior already)
+            const double* const lz = p.tail_lws + (inst >> 6) * p.tail_lws_block + (inst & 63);
+            for (int k = gl; k < N; k += G) {
 #pragma unroll
-            for (int j = 0; j < NY; ++j) {
-                double& y = j < NX ? sX[(k + 1) * NX + j] : sU[k * NU + j - NX];
-                y = ip_push(y, yl[j], yu[j]);
-                sZl[k * NY + j] = yl[j] > -INFINITY ? 1.0 : 0.0;
-                sZu[k * NY + j] = yu[j] < INFINITY ? 1.0 : 0.0;
+                for (int j = 0; j < NY; ++j) {
+                    sZl[k * NY + j] = lz[((int64_t)k * p.tail_lws_ss + p.tail_lws_zl + j) * 64];
+                    sZu[k * NY + j] = lz[((int64_t)k * p.tail_lws_ss + p.tail_lws_zl + NY + j) * 64];
+                }
+            }
+        } else {
+            // y pushed into the interior, z = 1 on finite bounds (oracle solve_one_ip)
+            for (int k = gl; k < N; k += G) {
+#pragma unroll
+                for (int j = 0; j < NY; ++j) {
+                    double& y = j < NX ? sX[(k + 1) * NX + j] : sU[k * NU + j - NX];
+                    y = ip_push(y, yl[j], yu[j]);
+                    sZl[k * NY + j] = yl[j] > -INFINITY ? 1.0 : 0.0;
+                    sZu[k * NY + j] = yu[j] < INFINITY ? 1.0 : 0.0;
+                }
             }
         }
     }

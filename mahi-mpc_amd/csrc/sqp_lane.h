@@ -63,6 +63,8 @@ namespace mmpc {
 __host__ __device__ constexpr int lane_stage_stride(int nx, int nu, bool xb = false) {
     return 5 * nx + 2 * nu + nu * (nx + nu + 1) + (xb ? 5 * (nx + nu) : 2 * nu + nx);
 }
+// field offset of the interior-point duals z_l (z_u follows at + nx + nu) in a stage (StageFields<.., true>::ZL)
+__host__ __device__ constexpr int lane_zl_offset(int nx, int nu) { return 5 * nx + 2 * nu + nu * (nx + nu + 1); }
 // linear-mode block: h-free Jacobian blocks da/dq (na x nq), da/dz (na x na), da/du (na x nu), xdot*, x*, u*
 __host__ __device__ constexpr int lane_lin_doubles(int nx, int nu, int nq) {
     return (nx - nq) * (nq + (nx - nq) + nu) + 2 * nx + nu;
@@ -98,6 +100,7 @@ struct StageFields {
     static constexpr int ZL = HOLD, ZU = ZL + NY, SG = ZU + NY, BB = SG + NY, ZG = BB + NY;
     static constexpr int SS = XB ? ZG + NY : U1 + NU;
     static_assert(SS == lane_stage_stride(NX, NU, XB), "layout");
+    static_assert(ZL == lane_zl_offset(NX, NU), "layout of the duals (state-bounded tail hand-over)");
 };
 
 struct LaneWork {
@@ -1007,8 +1010,8 @@ sqp_lane_kernel(SolveParams p,
                 // iterate, iteration count and merit weight -- the wave no longer waits for it.  At iteration
                 // tail_cap (and later, after an overflow), or earlier (from iteration 2) once at most tail_wave_max
                 // lanes of the wave are still iterating: the active lanes here are exactly the unconverged ones
-                bool hand = !BOUNDED && !XB && p.tail_cap > 0 && it >= p.tail_cap;
-                if (!BOUNDED && !XB && p.tail_cap > 0 && !hand && it >= 2 && p.tail_wave_max > 0)
+                bool hand = !BOUNDED && p.tail_cap > 0 && it >= p.tail_cap;
+                if (!BOUNDED && p.tail_cap > 0 && !hand && it >= 2 && p.tail_wave_max > 0)
                     hand = __popcll(__ballot(1)) <= p.tail_wave_max;
                 if (hand) {
                     const int slot = atomicAdd(p.tail_count, 1);
@@ -1016,6 +1019,7 @@ sqp_lane_kernel(SolveParams p,
                         p.tail_idx[slot] = (int32_t)inst;
                         p.tail_it[slot] = it;
                         p.tail_mu[slot] = mu;
+                        if constexpr (XB) p.tail_mub[slot] = mub;   // the duals stay in this launch's workspace
                         status = ST_HANDED_OVER;
                         done = true;
                         break;

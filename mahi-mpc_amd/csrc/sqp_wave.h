@@ -72,6 +72,13 @@ struct SolveParams {
     int32_t* tail_idx;     // [tail_slots] instance; in a 16-lane launch, non-null = resume launch over the list
     int32_t* tail_it;      // [tail_slots] iteration whose stop test failed
     double* tail_mu;       // [tail_slots] l1-merit penalty weight
+    double* tail_mub;      // [tail_slots] barrier parameter (state-bounded solves)
+    // state-bounded resume: the duals z_l, z_u stay in the handing-over lane launch's workspace (stage-major
+    // [64-instance block][stage][field][lane]); the resume launch's own workspace lies after it
+    const double* tail_lws;
+    int64_t tail_lws_block;  // doubles per 64-instance block
+    int tail_lws_ss;         // doubles per stage (x 64 lanes)
+    int tail_lws_zl;         // field offset of z_l; z_u follows at + nx + nu
     int gpw;               // 16-lane kernel: instance groups per wave of this launch (kGroupsPerWave, or fewer)
 };
 // instance status while handed over (never returned: the resume launch overwrites it)

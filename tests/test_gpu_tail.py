@@ -98,3 +98,35 @@ def test_tail_handover_wave_rule_loose_tolerance(mmpc_mod, oracle, tmp_path, mon
     assert (off["iters"] == r["iters"]).mean() >= 0.99
     same = off["iters"] == r["iters"]
     assert _rel(r["V"][same], off["V"][same]).max() <= 1e-10
+
+
+@pytest.mark.parametrize("model,wave,B", [("exo", 8, 512), ("exo", 40, 320), ("two_link", 24, 768)])
+def test_tail_handover_state_bounds(model, wave, B, mmpc_mod, oracle, tmp_path, monkeypatch):
+    """state-bounded (interior-point) lane solves hand over by the wave rule: the resume launch reads the duals from
+    the lane launch's workspace and continues with the same barrier parameter and merit weight -- same iterates as
+    without hand-over and as the oracle's interior-point solve (oracle solve_one_ip)"""
+    from conftest import WEIGHTS_CFG
+    if model == "exo":
+        nx, nu, N, w, mname, om = 8, 4, 50, W_EXO, "exo_arm", oracle.EXO
+        xl, xu = [-np.inf] * 4 + [-1.5] * 4, [np.inf] * 4 + [1.5] * 4
+    else:
+        nx, nu, N, w, mname, om = 4, 2, 30, np.array(WEIGHTS_CFG), "two_link_arm", oracle.TWO_LINK
+        xl, xu = [-np.inf] * 2 + [-1.5] * 2, [np.inf] * 2 + [1.5] * 2
+    x0, up, tr = oracle.synth(20250213, 9, B, N, H, model=om)
+
+    def solver(wave_max):
+        monkeypatch.setenv("MMPC_TAIL_WAVE", str(wave_max))
+        p = mmpc_mod.write_model_json(str(tmp_path / f"{model}_xb_{wave_max}.json"), model, nx, nu, 2000, N, model=mname)
+        s = mmpc_mod.Solver(p, kkt_solver=2, init_states=mmpc_mod.INIT_ZERO)
+        monkeypatch.delenv("MMPC_TAIL_WAVE")
+        s.set_state_bounds(xl, xu)
+        return s
+
+    r = solver(wave).solve_batch_host(x0, up, tr, w)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, model=om, kkt=oracle.KKT_RICCATI, init_states=2, x_lb=xl, x_ub=xu)
+    assert (r["status"] == 0).all() and (o["status"] == 0).all()
+    _compare(r, o)
+    off = solver(0).solve_batch_host(x0, up, tr, w)
+    assert (off["iters"] == r["iters"]).mean() >= 0.99
+    same = off["iters"] == r["iters"]
+    assert _rel(r["V"][same], off["V"][same]).max() <= 1e-10
