@@ -228,3 +228,21 @@ def test_rccl_is_loadable_for_the_multi_device_path(mmpc_mod):
     if not os.path.exists("/opt/rocm/lib/librccl.so.1"):
         pytest.skip("no librccl in this image")
     assert v >= 21000, v
+
+
+def test_reserve_workspace_bytes_include_the_tail_hand_over(tmp_path, mmpc_mod):
+    """mmpc_reserve_workspace reports its size before touching a device: the solver workspace, the iteration-tail
+    hand-over list and, for state-bounded solves, the resume launch's own workspace (sized for 256 CUs
+    until a device was queried)"""
+    p = mmpc_mod.write_model_json(str(tmp_path / "exo.json"), "exo", 8, 4, 2000, 50, model="exo_arm")
+    s = mmpc_mod.Solver(p)
+    b = C.c_uint64(0)
+    s._L.mmpc_reserve_workspace(s._h, 65536, C.byref(b))   # no GPU here: an error code, the size set before it
+    plain = b.value
+    assert plain > 256 + 65536 * 24
+    s.set_state_bounds([-np.inf] * 4 + [-1.5] * 4, [np.inf] * 4 + [1.5] * 4)
+    s._L.mmpc_reserve_workspace(s._h, 65536, C.byref(b))
+    assert b.value > plain and (b.value - plain) % 8 == 0
+    s.set_state_bounds(None, None)
+    s._L.mmpc_reserve_workspace(s._h, 65536, C.byref(b))
+    assert b.value == plain
