@@ -105,8 +105,9 @@ enum mmpc_kkt_solver {
                                nonlinear solves of models with nx+nu < 16 hand instances still unconverged after
                                iteration 4 (or once at most 8 lanes of their wave are left) to a 16-lane resume
                                launch on the same stream that continues the same iterates; with
-                               factor_fp32 that tail runs the fp64 factor; state-bounded solves hand over by the
-                               wave rule (4 lanes) with their duals and barrier parameter.  Env MMPC_TAIL_CAP / MMPC_TAIL_WAVE /
+                               factor_fp32 that tail runs the fp64 factor; bounded solves hand over by the wave
+                               rule alone (4 lanes), with their duals and barrier parameter (state bounds) or the
+                               lane kernel's active-set rule (control bounds).  Env MMPC_TAIL_CAP / MMPC_TAIL_WAVE /
                                MMPC_TAIL_ROUNDS, read at mmpc_create (0 = off), override the policy */
     MMPC_KKT_RICCATI_GROUP = 3 /* 16 lanes per instance: stage-parallel model evaluations and line search,
                                   serial Riccati sweeps from LDS (stage data of 4 instances <= 160 KB LDS) */

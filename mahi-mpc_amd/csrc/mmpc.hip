@@ -760,9 +760,10 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
 // Hessian; 3 hands over too many: cfg#3 12.8 ms), MMPC_TAIL_CAP overrides (0 = off). slots: four rounds of resume
 // workgroups (groups per workgroup gpw with <= 64 KB of LDS, up to 4 one-wave workgroups per CU per round),
 // MMPC_TAIL_ROUNDS overrides.
-// State-bounded (interior-point) solves hand over by the wave rule alone (their counts spread over 10-21 iterations
-// at the exo's cfg#3 size: no common cap), the duals read from the lane launch's workspace by the resume launch,
-// whose own workspace then lies after the hand-over list (xb_ws_bytes).
+// Bounded solves hand over by the wave rule alone (their counts spread: no common cap). State bounds: the duals are
+// read from the lane launch's workspace by the resume launch, whose own workspace then lies after the hand-over list
+// (xb_ws_bytes). Control bounds: the resume launch runs the lane kernel's active-set rule (no_release) from the
+// handed-over hold epsilon (tail_mub).
 struct TailPlan {
     int cap = 0, wave_max = 0, slots = 0, gpw = 1;
     size_t lds = 0, xb_ws_bytes = 0;
@@ -771,18 +772,22 @@ TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded, int
     TailPlan t;
     const mmpc_model_info& mi = h->info;
     const bool xb = p.x_bounded != 0;
-    if ((bounded && !xb) || mi.is_linear || p.trace || cu <= 0) return t;
+    if (mi.is_linear || p.trace || cu <= 0) return t;
     if (mi.num_x + mi.num_u >= kGroupLanes) return t;
     constexpr int kNoCap = 1 << 20;
-    const int cap = h->tail_cap_env >= 0 ? h->tail_cap_env : (xb ? kNoCap : 4);
-    if (cap <= 0 || (cap >= p.max_iter && !xb)) return t;
-    // wave rule threshold: 8 lanes (Gauss-Newton / exact: only the thin tails of loose tolerances use it), 4 for
-    // interior-point solves, whose handed-over instances need several more iterations (exo |qdot| <= 1.5 at cfg#3
-    // size: 65.3 ms without, 62.2 / 61.0 / 61.0 / 60.5 / 67.6 ms at 1 / 2 / 3 / 4 / 6, profiles/r05/xbwave)
-    const int wave_max = h->tail_wave_env >= 0 ? h->tail_wave_env : (xb ? 4 : 8);
-    if (xb && cap >= p.max_iter && wave_max <= 0) return t;
-    const size_t inst = static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, h->nq, mi.num_shooting_nodes, false,
-                                                              false, xb)) * sizeof(double);
+    // bounded solves (state: interior point; control: projected SQP with its QP re-solves) hand over by the wave rule
+    // alone: their counts spread (exo |u| <= 0.5: 4.3 mean, 12 max), and a cap either hands over too many or none
+    const bool spread = xb || bounded;
+    const int cap = h->tail_cap_env >= 0 ? h->tail_cap_env : (spread ? kNoCap : 4);
+    if (cap <= 0 || (cap >= p.max_iter && !spread)) return t;
+    // wave rule threshold: 8 lanes (unbounded: only the thin tails of loose tolerances use it), 4 for bounded solves,
+    // whose handed-over instances need several more iterations (exo at cfg#3 size, ms without / with 4: |qdot| <= 1.5
+    // 65.3 / 60.5 (1 / 2 / 3 / 6 lanes: 62.2 / 61.0 / 61.0 / 67.6, profiles/r05/xbwave); |u| <= 0.5 36.9 / 30.1, |u| <= 2
+    // 22.7 / 22.2 (8 lanes: 38.4 / 21.0; caps 4-8 beside it, profiles/r05/ubsweep))
+    const int wave_max = h->tail_wave_env >= 0 ? h->tail_wave_env : (spread ? 4 : 8);
+    if (spread && cap >= p.max_iter && wave_max <= 0) return t;
+    const size_t inst = static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, h->nq, mi.num_shooting_nodes,
+                                                              bounded && !xb, false, xb)) * sizeof(double);
     if (inst > 64 * 1024) return t;
     const int gpw = static_cast<int>(std::max<size_t>(1, std::min<size_t>(kGroupsPerWave, (64 * 1024) / inst)));
     const int per_cu = static_cast<int>(std::min<size_t>(4, (160 * 1024) / (gpw * inst)));
@@ -849,6 +854,7 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.tail_count = p.tail_idx = p.tail_it = nullptr;
     p.tail_mu = p.tail_mub = nullptr;
     p.tail_lws = nullptr;
+    p.no_release = 0;
     p.tail_lws_block = 0;
     p.tail_lws_ss = p.tail_lws_zl = 0;
     p.gpw = kGroupsPerWave;
@@ -962,7 +968,9 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
             pr.tail_cap = 0;
             pr.gpw = tp.gpw;
             pr.init_hold = pr.init_zero = 0;   // the handed-over iterate is in V
+            pr.no_release = 1;                 // control bounds: the lane kernel's active-set rule
             const bool xb = p.x_bounded != 0;
+            const bool ub = bounded && !xb;
             GroupWork gwk{lw.ws};
             if (xb) {   // duals from the lane workspace; the resume workspace after the hand-over list
                 const int nx = mi.num_x, nu = mi.num_u, N = mi.num_shooting_nodes;
@@ -977,18 +985,21 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
                 using M = std::remove_pointer_t<decltype(m)>;
                 if constexpr (M::NX + M::NU < kGroupLanes) {
                     if constexpr (std::is_same<M, TwoLinkArm>::value) {
+                        const bool ex = hess == MMPC_HESSIAN_EXACT;
                         const hipError_t e =
-                            xb ? launch_group_two_link_bounded(true, false, rgrid, rblock, tp.lds, stream, pr, gwk)
-                               : launch_group_two_link(hess == MMPC_HESSIAN_EXACT, rgrid, rblock, tp.lds, stream, pr, gwk);
+                            (xb || ub) ? launch_group_two_link_bounded(xb, ex && !xb, rgrid, rblock, tp.lds, stream, pr, gwk)
+                                       : launch_group_two_link(ex, rgrid, rblock, tp.lds, stream, pr, gwk);
                         return e == hipSuccess ? MMPC_OK : fail(MMPC_ERR_HIP, std::string("resume launch: ") +
                                                                                   hipGetErrorString(e));
                     } else {
                         if (xb) return launch_group<M, false, true>(rgrid, rblock, tp.lds, stream, pr, gwk);
                         if constexpr (exact_capable<M>()) {
                             if (hess == MMPC_HESSIAN_EXACT)
-                                return launch_group<M, false, false, true>(rgrid, rblock, tp.lds, stream, pr, gwk);
+                                return ub ? launch_group<M, true, false, true>(rgrid, rblock, tp.lds, stream, pr, gwk)
+                                          : launch_group<M, false, false, true>(rgrid, rblock, tp.lds, stream, pr, gwk);
                         }
-                        return launch_group<M, false>(rgrid, rblock, tp.lds, stream, pr, gwk);
+                        return ub ? launch_group<M, true>(rgrid, rblock, tp.lds, stream, pr, gwk)
+                                  : launch_group<M, false>(rgrid, rblock, tp.lds, stream, pr, gwk);
                     }
                 } else {
                     return fail(MMPC_ERR_UNSUPPORTED, "tail hand-over: nx + nu >= 16");   // tail_plan excludes it

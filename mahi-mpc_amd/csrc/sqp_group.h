@@ -339,7 +339,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     __builtin_amdgcn_wave_barrier();
     int status = ST_MAX_ITER;
     int it = 0;
-    double kkt = 0.0, mu = resume ? p.tail_mu[slot] : 0.0, pg_prev = INFINITY;
+    double kkt = 0.0, mu = resume ? p.tail_mu[slot] : 0.0, pg_prev = (BOUNDED && resume) ? p.tail_mub[slot] : INFINITY;
     bool done = !valid;
     // FUSE_FWD: the line search's alpha = 1 trial evaluates the model with its Jacobian and writes everything phase A
     // computes at that point (F_k, c_k, the stage blocks; J, |c|_1, max|c|); when the full step is accepted (every
@@ -1576,7 +1576,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                                     sHold[k * NU + ru] = t < lbr ? lbr : ubr;
                                     resolve = true;
                                 }
-                            } else {   // held: release it when its multiplier H_ww du + [H_wx | -R] s + h_w points inward
+                            } else if (!p.no_release) {   // held: release it when its multiplier H_ww du + [H_wx | -R] s + h_w points inward
                                 double m = o.Rw[NR - 1];
 #pragma unroll
                                 for (int j = 0; j < NS; ++j) m = fma(o.Rw[j], sb[j], m);
@@ -1640,7 +1640,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 resolve = false;
                 // QP solves of this iteration: two at the first (the cold start's active set moves most there, and a
                 // wave pays its slowest instance's solves), kBoundPasses later (oracle bound_release)
-                const int passes = it == 0 ? 2 : kBoundPasses;
+                const int passes = (it == 0 && !p.no_release) ? 2 : kBoundPasses;
                 step_dist(BOUNDED && pass + 1 < passes);
                 if constexpr (!BOUNDED) {
                     break;

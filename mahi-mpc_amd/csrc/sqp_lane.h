@@ -1010,8 +1010,8 @@ sqp_lane_kernel(SolveParams p,
                 // iterate, iteration count and merit weight -- the wave no longer waits for it.  At iteration
                 // tail_cap (and later, after an overflow), or earlier (from iteration 2) once at most tail_wave_max
                 // lanes of the wave are still iterating: the active lanes here are exactly the unconverged ones
-                bool hand = !BOUNDED && p.tail_cap > 0 && it >= p.tail_cap;
-                if (!BOUNDED && p.tail_cap > 0 && !hand && it >= 2 && p.tail_wave_max > 0)
+                bool hand = p.tail_cap > 0 && it >= p.tail_cap;
+                if (p.tail_cap > 0 && !hand && it >= 2 && p.tail_wave_max > 0)
                     hand = __popcll(__ballot(1)) <= p.tail_wave_max;
                 if (hand) {
                     const int slot = atomicAdd(p.tail_count, 1);
@@ -1020,6 +1020,7 @@ sqp_lane_kernel(SolveParams p,
                         p.tail_it[slot] = it;
                         p.tail_mu[slot] = mu;
                         if constexpr (XB) p.tail_mub[slot] = mub;   // the duals stay in this launch's workspace
+                        if constexpr (BOUNDED) p.tail_mub[slot] = pg_prev;   // the epsilon of the hold rule
                         status = ST_HANDED_OVER;
                         done = true;
                         break;

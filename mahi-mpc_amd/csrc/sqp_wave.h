@@ -72,7 +72,8 @@ struct SolveParams {
     int32_t* tail_idx;     // [tail_slots] instance; in a 16-lane launch, non-null = resume launch over the list
     int32_t* tail_it;      // [tail_slots] iteration whose stop test failed
     double* tail_mu;       // [tail_slots] l1-merit penalty weight
-    double* tail_mub;      // [tail_slots] barrier parameter (state-bounded solves)
+    double* tail_mub;      // [tail_slots] barrier parameter (state bounds) / previous projected gradient (control bounds)
+    int no_release;        // 16-lane BOUNDED: holds are only added, kBoundPasses QP solves (the lane kernel's rule)
     // state-bounded resume: the duals z_l, z_u stay in the handing-over lane launch's workspace (stage-major
     // [64-instance block][stage][field][lane]); the resume launch's own workspace lies after it
     const double* tail_lws;

@@ -130,3 +130,36 @@ def test_tail_handover_state_bounds(model, wave, B, mmpc_mod, oracle, tmp_path, 
     assert (off["iters"] == r["iters"]).mean() >= 0.99
     same = off["iters"] == r["iters"]
     assert _rel(r["V"][same], off["V"][same]).max() <= 1e-10
+
+
+@pytest.mark.parametrize("model,ub,cap,B,hess", [("exo", 0.5, 3, 640, 1), ("exo", 2.0, 2, 512, 2),
+                                                 ("two_link", 2.0, 3, 768, 1)])
+def test_tail_handover_control_bounds(model, ub, cap, B, hess, mmpc_mod, oracle, tmp_path, monkeypatch):
+    """control-bounded (projected SQP) lane solves: the resume launch runs the 16-lane kernel with the lane kernel's
+    active-set rule (holds only added, four QP solves; SolveParams.no_release) from the handed-over iterate, merit
+    weight and hold epsilon -- same iterates as the oracle's projected SQP without releases and as no hand-over"""
+    from conftest import WEIGHTS_CFG
+    if model == "exo":
+        nx, nu, N, w, mname, om = 8, 4, 50, W_EXO, "exo_arm", oracle.EXO
+    else:
+        nx, nu, N, w, mname, om = 4, 2, 30, np.array(WEIGHTS_CFG), "two_link_arm", oracle.TWO_LINK
+    lb, ubv = [-ub] * nu, [ub] * nu
+    x0, up, tr = oracle.synth(20250213, 17, B, N, H, model=om)
+
+    def solver(c):
+        monkeypatch.setenv("MMPC_TAIL_CAP", str(c))
+        p = mmpc_mod.write_model_json(str(tmp_path / f"{model}_ub_{c}.json"), model, nx, nu, 2000, N, model=mname)
+        s = mmpc_mod.Solver(p, kkt_solver=2, init_states=mmpc_mod.INIT_ZERO, hessian=hess)
+        monkeypatch.delenv("MMPC_TAIL_CAP")
+        return s
+
+    s = solver(cap)
+    r = s.solve_batch_host(x0, up, tr, w, u_lb=lb, u_ub=ubv)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, model=om, u_lb=lb, u_ub=ubv, init_states=2, solver=s)
+    assert (r["iters"] > cap).sum() > 0
+    np.testing.assert_array_equal(r["status"], o["status"])
+    _compare(r, o)
+    off = solver(0).solve_batch_host(x0, up, tr, w, u_lb=lb, u_ub=ubv)
+    assert (off["iters"] == r["iters"]).mean() >= 0.99
+    same = off["iters"] == r["iters"]
+    assert _rel(r["V"][same], off["V"][same]).max() <= 1e-10
