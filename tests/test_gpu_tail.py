@@ -163,3 +163,24 @@ def test_tail_handover_control_bounds(model, ub, cap, B, hess, mmpc_mod, oracle,
     assert (off["iters"] == r["iters"]).mean() >= 0.99
     same = off["iters"] == r["iters"]
     assert _rel(r["V"][same], off["V"][same]).max() <= 1e-10
+
+
+@pytest.mark.parametrize("B", [1, 3, 65])
+def test_tail_handover_tiny_and_ragged_batches(B, mmpc_mod, oracle, tmp_path, monkeypatch):
+    """one partial wave (B < 64) and a ragged last wave (65): the wave rule counts only the lanes of real instances
+    (the others left the kernel at its first line), the resume launch's slots are clamped to B -- unbounded and
+    state-bounded exo lane solves, against the oracle"""
+    N = 50
+    x0, up, tr = oracle.synth(20250213, 31, B, N, H, model=oracle.EXO)
+    s = _solve(mmpc_mod, tmp_path, monkeypatch, 4, B)
+    r = s.solve_batch_host(x0, up, tr, W_EXO)
+    o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, model=oracle.EXO, kkt=oracle.KKT_RICCATI, init_states=2)
+    assert (r["status"] == 0).all()
+    _compare(r, o)
+    xl, xu = [-np.inf] * 4 + [-1.5] * 4, [np.inf] * 4 + [1.5] * 4
+    s.set_state_bounds(xl, xu)
+    r = s.solve_batch_host(x0, up, tr, W_EXO)
+    o = oracle.solve_batch(N, H, x0, up, tr, W_EXO, model=oracle.EXO, kkt=oracle.KKT_RICCATI, init_states=2,
+                           x_lb=xl, x_ub=xu)
+    assert (r["status"] == 0).all()
+    _compare(r, o)
