@@ -57,13 +57,15 @@ CONFIGS = {
                           "||grad||<=1e-8, ||g||<=1e-10"),
     "cfg3": dict(model="exo_arm", nx=8, nu=4, N=50, B=65536, weights=WEIGHTS_EXO, metric=_EXO_METRIC, fp32=False,
                  workload="cfg#3: 4-DoF exo nx=8 nu=4 (build-defined parameters), N=50, h=2 ms, cold-start GN-SQP "
-                          "(Riccati KKT) to ||grad||<=1e-8, ||g||<=1e-10"),
+                          "(Riccati KKT, lane per instance; instances unconverged after iteration 4 continue in a "
+                          "16-lane resume launch, same iterates) to ||grad||<=1e-8, ||g||<=1e-10"),
     "cfg5": dict(model="exo_arm", nx=8, nu=4, N=50, B=65536, weights=WEIGHTS_EXO, fp32=True,
                  metric="MPC solves/sec (whole node), exo nx=8 N=50 batch, fp32 KKT factor + fp64 residuals "
                         "(SURVEY.md 8d cfg#5)",
                  workload="cfg#5: cfg#3 with the Riccati matrix recursion in fp32 and every right-hand side, "
                           "residual, model evaluation and merit in fp64 (each SQP iteration = one refinement "
-                          "step), to ||grad||<=1e-8, ||g||<=1e-10"),
+                          "step; the iteration tail continues with the fp64 factor in the 16-lane resume launch), "
+                          "to ||grad||<=1e-8, ||g||<=1e-10"),
 }
 FP64_PEAK_TFLOPS = 78.6   # MI355X FP64 vector peak (AMD spec); FP64 matrix peak is the same
 FP32_PEAK_TFLOPS = 157.3  # MI355X FP32 vector peak (MI355X_MICROARCH.md chip table)
