@@ -1823,6 +1823,10 @@ const char* mmpc_last_error(void) { return g_last_error.c_str(); }
 
 // Internal diagnostic: per-phase s_memtime cycle totals of the SQP kernel (all zero unless the library
 // was built with -DMMPC_PHASE_TIMING, i.e. lib/libmmpc_timing.so).  out[15] = number of waves.
+// sums, except slots 10-12 (latest end, ~earliest start, longest wave: sqp_wave.h MMPC_PHASE_FLUSH), which are maxima
+static void merge_phase_tables(unsigned long long* out16, const unsigned long long* t) {
+    for (int i = 0; i < 16; ++i) out16[i] = (i >= 10 && i <= 12) ? std::max(out16[i], t[i]) : out16[i] + t[i];
+}
 int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) {
     if (!out16) return fail(MMPC_ERR_INVALID_ARG, "null");
     MMPC_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mmpc_phase_cycles), 16 * sizeof(unsigned long long)));
@@ -1832,12 +1836,12 @@ int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) {
     }
     unsigned long long lane[16];   // the lane kernels' table lives in their own translation unit (lane_launch.h)
     MMPC_HIP(lane_phase_cycles(lane, reset != 0));
-    for (int i = 0; i < 16; ++i) out16[i] += lane[i];
+    merge_phase_tables(out16, lane);
 #if MMPC_BUILTIN_MODELS
     MMPC_HIP(group_two_link_phase_cycles(lane, reset != 0));   // the 2-link group kernels' units (group_launch.h)
-    for (int i = 0; i < 16; ++i) out16[i] += lane[i];
+    merge_phase_tables(out16, lane);
     MMPC_HIP(group_two_link_bounded_phase_cycles(lane, reset != 0));
-    for (int i = 0; i < 16; ++i) out16[i] += lane[i];
+    merge_phase_tables(out16, lane);
 #endif
     return MMPC_OK;
 }

@@ -418,6 +418,7 @@ sqp_lane_kernel(SolveParams p,
     bool fwd_ready = false;
     double J0n = 0.0, c1n = 0.0, cmaxn = 0.0;
     bool nfn = false;
+    bool lean_off = false;   // a hand-over of this instance found the list full: no lean sweeps, no further claims
     MMPC_PHASE(0);
     #pragma unroll 1
     for (it = 0; it <= p.max_iter; ++it) {
@@ -532,6 +533,128 @@ sqp_lane_kernel(SolveParams p,
         bool nft1 = false;
         // diagnostic trace [B][max_iter+1][8] = (||2g||, ||c||, J, |c|_1, dJ, alpha, mu, ||lam||)
         double* trc = p.trace ? p.trace + (inst * (p.max_iter + 1) + it) * 8 : nullptr;
+        // ---- (2') lean sweep (round 6): when every lane of the wave leaves at this iteration's stop test -- it converges,
+        // or it is handed over to the resume launch (the rule of the stop test below: `it` and the number of lanes still
+        // iterating, both known before the sweep; the lanes that converge at this test are counted here too, so the
+        // count is an upper bound of the stop test's), or the iteration limit is reached -- the backward sweep forms only
+        // the adjoint, the reduced gradient and the stop test: the Riccati step's gains would never be read (the resume
+        // launch solves its own QP).  Same expressions and order as sweep (2), so gmax / lmax / nonfinite are its values
+        // bit for bit.  An instance whose hand-over finds the list full (lean_off) continues into the full sweep below,
+        // which recomputes them.  At cfg#3 this is the wave's last backward sweep (iteration 4: every unconverged lane
+        // is handed over at the cap).
+        if (!lean_off && it >= 1 &&
+            (it == p.max_iter || (p.tail_cap > 0 && (it >= p.tail_cap || (it >= 2 && p.tail_wave_max > 0 &&
+                                                                           __popcll(__ballot(1)) <= p.tail_wave_max))))) {
+            double lam[NX], unext[NU], xpf[NX], upf[NU];
+#pragma unroll
+            for (int r = 0; r < NX; ++r) {
+                const double eb = ST(N, FX, r) - ST(N - 1, SF::R, r);  // x_N - r_{N-1}
+                lam[r] = Q[r] * (ST(N, SF::D, r) + eb);                // lam_N = Q e_{N-1}
+                if constexpr (XB) lam[r] += ST(N - 1, SF::ZG, r);
+                lmax = fmax(lmax, fabs(lam[r]));
+                xpf[r] = ST(N - 1, FX, r);
+            }
+#pragma unroll
+            for (int c = 0; c < NU; ++c) {
+                unext[c] = 0.0;
+                upf[c] = ST(N - 1, FU, c);
+            }
+            #pragma unroll 1
+            for (int k = N - 1; k >= 0; --k) {
+                gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
+                double x[NX], u[NU], um[NU], dk[NX], rkm[NX], xd[NX], hFq[SQ], hFqd[NA * NA], hFu[NA * NU];
+                double zgu[XB ? NU : 1], zgx[XB ? NX : 1];
+#pragma unroll
+                for (int r = 0; r < NX; ++r) {
+                    x[r] = xpf[r];
+                    dk[r] = SK(0, SF::D, r);
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) u[c] = upf[c];
+                if (k >= 1) {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        rkm[r] = SK(-1, SF::R, r);
+                        xpf[r] = SK(-1, FX, r);
+                    }
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) um[c] = SK(-1, FU, c);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) rkm[r] = 0.0;
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) um[c] = up[c];
+                }
+#pragma unroll
+                for (int c = 0; c < NU; ++c) upf[c] = um[c];
+                if constexpr (XB) {
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) zgu[c] = SK(0, SF::ZG, NX + c);
+                    if (k >= 1) {
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) zgx[r] = SK(-1, SF::ZG, r);
+                    }
+                }
+                STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+#pragma unroll
+                for (int c = 0; c < NU; ++c) {   // reduced gradient, as sweep (2)
+                    double g = 0.0;
+#pragma unroll
+                    for (int s = 0; s < NA; ++s) g = fma(hFu[s * NU + c], lam[NQ + s], g);
+                    g = fma(R[c], u[c] - um[c], fma(Rm[c], u[c], g));
+                    if (k + 1 < N) g -= R[c] * (unext[c] - u[c]);
+                    if constexpr (XB) g += zgu[c];
+                    if (!BOUNDED) gmax = fmax(gmax, fabs(2.0 * g));
+                    else gmax = fmax(gmax, fabs(u[c] - proj(u[c] - 2.0 * g, lbv[c], ubv[c])));
+                    nonfinite |= !isfinite(g);
+                    unext[c] = u[c];
+                }
+                if (k >= 1) {   // adjoint, as sweep (2)
+                    double ln[NX];
+                    at_mul<NQ, NA>(h, hFq, hFqd, lam, ln);
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) {
+                        lam[r] = fma(Q[r], dk[r] + x[r] - rkm[r], ln[r]);
+                        if constexpr (XB) lam[r] += zgx[r];
+                        lmax = fmax(lmax, fabs(lam[r]));
+                    }
+                }
+            }
+            kkt = fmax(gmax, cmax);
+            if (XB) kkt = fmax(kkt, 2.0 * cmpl0);
+            if (trc) {
+                trc[0] = gmax;
+                trc[1] = cmax;
+                trc[2] = J0;
+                trc[3] = c1;
+                trc[7] = lmax;
+            }
+            if (nonfinite || !isfinite(kkt)) {
+                status = ST_NONFINITE;
+                break;
+            }
+            if (gmax <= p.tol_grad && cmax <= p.tol_defect && (!XB || 2.0 * cmpl0 <= kIpTolCompl)) {
+                status = ST_CONVERGED;
+                break;
+            }
+            if (it == p.max_iter) {
+                status = ST_MAX_ITER;
+                break;
+            }
+            const int slot = atomicAdd(p.tail_count, 1);   // the hand-over of the stop test below
+            if (slot < p.tail_slots) {
+                p.tail_idx[slot] = (int32_t)inst;
+                p.tail_it[slot] = it;
+                p.tail_mu[slot] = mu;
+                if constexpr (XB) p.tail_mub[slot] = mub;
+                if constexpr (BOUNDED) p.tail_mub[slot] = pg_prev;
+                status = ST_HANDED_OVER;
+                break;
+            }
+            lean_off = true;   // list full: the overflow path (the full sweep and the rest of this iteration)
+            gmax = 0.0;
+            lmax = 0.0;
+        }
         // exact-Hessian blocks in this iteration's sweeps; false after a sweep's exact QP was not positive definite:
         // that sweep is redone and, with control bounds, every later QP solve of the iteration stays Gauss-Newton
         // (oracle solve_one: gn_fallback)
@@ -1010,8 +1133,8 @@ sqp_lane_kernel(SolveParams p,
                 // iterate, iteration count and merit weight -- the wave no longer waits for it.  At iteration
                 // tail_cap (and later, after an overflow), or earlier (from iteration 2) once at most tail_wave_max
                 // lanes of the wave are still iterating: the active lanes here are exactly the unconverged ones
-                bool hand = p.tail_cap > 0 && it >= p.tail_cap;
-                if (p.tail_cap > 0 && !hand && it >= 2 && p.tail_wave_max > 0)
+                bool hand = p.tail_cap > 0 && !lean_off && it >= p.tail_cap;   // lean_off: the list is full
+                if (p.tail_cap > 0 && !lean_off && !hand && it >= 2 && p.tail_wave_max > 0)
                     hand = __popcll(__ballot(1)) <= p.tail_wave_max;
                 if (hand) {
                     const int slot = atomicAdd(p.tail_count, 1);
@@ -1025,6 +1148,7 @@ sqp_lane_kernel(SolveParams p,
                         done = true;
                         break;
                     }
+                    lean_off = true;
                 }
                 if (BOUNDED) pg_prev = gmax;
                 // barrier update for the next iteration (IPOPT monotone rule, lagged; oracle solve_one_ip)

@@ -291,7 +291,12 @@ __device__ __forceinline__ double rcp_nr(double a) {
 // Only the diagnostic library libmmpc_timing.so is built with it; its run time is not quoted.
 __device__ unsigned long long g_mmpc_phase_cycles[16];
 #ifdef MMPC_PHASE_TIMING
-#define MMPC_PHASE_DECL unsigned long long ph_acc[10] = {0}, ph_t = __builtin_amdgcn_s_memtime();
+// Slots 10-14 (round 6): the wave's wall-clock extent from s_memrealtime (100 MHz) -- 10: latest end, 11: ~earliest
+// start (atomicMax of the complement), 12: longest wave, 13: sum of wave durations, 14: sum of shader cycles (s_memtime)
+// over the same extents, so that cycles / duration gives the clock the waves ran at.
+#define MMPC_PHASE_DECL                                                                            \
+    unsigned long long ph_acc[10] = {0}, ph_t = __builtin_amdgcn_s_memtime(), ph_m0 = ph_t,        \
+                       ph_r0 = __builtin_amdgcn_s_memrealtime();
 #define MMPC_PHASE(i)                                        \
     do {                                                     \
         __builtin_amdgcn_sched_barrier(0);                   \
@@ -300,10 +305,17 @@ __device__ unsigned long long g_mmpc_phase_cycles[16];
         ph_t = t_;                                           \
         __builtin_amdgcn_sched_barrier(0);                   \
     } while (0)
-#define MMPC_PHASE_FLUSH                                                          \
-    if (lane0 == 0) {                                                             \
-        for (int q_ = 0; q_ < 10; ++q_) atomicAdd(&g_mmpc_phase_cycles[q_], ph_acc[q_]); \
-        atomicAdd(&g_mmpc_phase_cycles[15], 1ull);                                \
+#define MMPC_PHASE_FLUSH                                                                   \
+    if (lane0 == 0) {                                                                      \
+        const unsigned long long r1_ = __builtin_amdgcn_s_memrealtime(),                   \
+                                 m1_ = __builtin_amdgcn_s_memtime();                       \
+        for (int q_ = 0; q_ < 10; ++q_) atomicAdd(&g_mmpc_phase_cycles[q_], ph_acc[q_]);   \
+        atomicMax(&g_mmpc_phase_cycles[10], r1_);                                          \
+        atomicMax(&g_mmpc_phase_cycles[11], ~ph_r0);                                       \
+        atomicMax(&g_mmpc_phase_cycles[12], r1_ - ph_r0);                                  \
+        atomicAdd(&g_mmpc_phase_cycles[13], r1_ - ph_r0);                                  \
+        atomicAdd(&g_mmpc_phase_cycles[14], m1_ - ph_m0);                                  \
+        atomicAdd(&g_mmpc_phase_cycles[15], 1ull);                                         \
     }
 #else
 #define MMPC_PHASE_DECL

@@ -29,6 +29,8 @@ ap.add_argument("--kkt", type=int, default=0, help="kkt_solver (0 auto, 1 conden
 ap.add_argument("--u-bound", type=float, default=None, help="control bounds |u| <= U (projected SQP)")
 ap.add_argument("--hessian", type=int, default=0, help="mmpc_opts.hessian (0 auto, 1 Gauss-Newton, 2 exact)")
 ap.add_argument("--x-bound", type=float, default=None, help="state bounds |qdot| <= X (interior point)")
+ap.add_argument("--tol-grad", type=float, default=None, help="mmpc_opts.tol_grad (default 1e-8)")
+ap.add_argument("--tol-defect", type=float, default=None, help="mmpc_opts.tol_defect (default 1e-10)")
 a = ap.parse_args()
 exo = a.config == "cfg3"
 B = a.batch or (65536 if exo else 4096)
@@ -37,7 +39,7 @@ nx, nu = (8, 4) if exo else (4, 2)
 L = mmpc.lib()
 L.mmpc_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
 path = mmpc.write_model_json("/tmp/mmpc_phase.json", "phase", nx, nu, 2000, N)
-s = mmpc.Solver(path, kkt_solver=a.kkt, hessian=a.hessian)
+s = mmpc.Solver(path, kkt_solver=a.kkt, hessian=a.hessian, tol_grad=a.tol_grad, tol_defect=a.tol_defect)
 if a.x_bound is not None:
     s.set_state_bounds([-np.inf] * (nx // 2) + [-a.x_bound] * (nx // 2), [np.inf] * (nx // 2) + [a.x_bound] * (nx // 2))
 NAMES_GROUP = ["load", "A:evals(parallel)", "B:d+adjoint(+riccati if not DIST)", "riccati(DIST)+mu",
@@ -66,8 +68,18 @@ L.mmpc_debug_phase_cycles(buf, 1)
 cyc = np.array(buf[:10], dtype=np.float64)
 waves = buf[15]
 iters = it.cpu().numpy()
-out = {"config": a.config, "u_bound": a.u_bound, "x_bound": a.x_bound, "hessian": s.hessian_for(B, a.u_bound is not None), "waves": int(waves), "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
+out = {"config": a.config, "tol_grad": a.tol_grad, "tol_defect": a.tol_defect, "u_bound": a.u_bound, "x_bound": a.x_bound, "hessian": s.hessian_for(B, a.u_bound is not None), "waves": int(waves), "mean_iters": float(iters.mean()), "max_iters": int(iters.max()),
+       "iters_hist": {int(k): int(v) for k, v in zip(*np.unique(iters, return_counts=True))},
+       # a wave runs until its slowest instance: 4 instances per wave (16-lane kernel) or 64 (lane kernel)
+       "wave_max_iters_mean": float(iters[: B // (4 if ksolver == 3 else 64) * (4 if ksolver == 3 else 64)]
+                                    .reshape(-1, 4 if ksolver == 3 else 64).max(1).mean()),
        "cycles_per_wave": float(cyc.sum() / waves),
+       # wall-clock extents (s_memrealtime, 100 MHz): the kernel's span from the first wave start to the last wave end,
+       # the longest and the mean wave, and the mean shader clock of the waves (s_memtime cycles / duration)
+       "span_us": float((buf[10] - (~buf[11] & 0xFFFFFFFFFFFFFFFF)) / 100.0),
+       "longest_wave_us": float(buf[12] / 100.0),
+       "mean_wave_us": float(buf[13] / 100.0 / waves),
+       "mean_clock_ghz": float(buf[14] / buf[13] * 0.1) if buf[13] else None,
        "per_phase_cycles_per_wave_iteration": {n: float(c / waves / (iters.mean() + 1)) for n, c in zip(NAMES, cyc)},
        "share": {n: float(c / cyc.sum()) for n, c in zip(NAMES, cyc)}}
 print(json.dumps(out, indent=1))
