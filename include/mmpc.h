@@ -58,7 +58,7 @@
 extern "C" {
 #endif
 
-#define MMPC_ABI_VERSION 5
+#define MMPC_ABI_VERSION 6
 
 typedef struct mmpc_handle mmpc_handle;
 
@@ -107,8 +107,7 @@ enum mmpc_kkt_solver {
                                launch on the same stream that continues the same iterates; with
                                factor_fp32 that tail runs the fp64 factor; bounded solves hand over by the wave
                                rule alone (4 lanes), with their duals and barrier parameter (state bounds) or the
-                               lane kernel's active-set rule (control bounds).  Env MMPC_TAIL_CAP / MMPC_TAIL_WAVE /
-                               MMPC_TAIL_ROUNDS, read at mmpc_create (0 = off), override the policy */
+                               lane kernel's active-set rule (control bounds).  Policy: opts.tail_* (ABI 6) */
     MMPC_KKT_RICCATI_GROUP = 3 /* 16 lanes per instance: stage-parallel model evaluations and line search,
                                   serial Riccati sweeps from LDS (stage data of 4 instances <= 160 KB LDS) */
 };
@@ -154,6 +153,19 @@ typedef struct mmpc_opts {
                             cfg#5; each SQP iteration refines the fp32 step). Riccati solver only. default 0 */
     int32_t init_states; /* enum mmpc_init_states. default MMPC_INIT_AS_GIVEN */
     int32_t hessian;     /* enum mmpc_hessian. default MMPC_HESSIAN_AUTO (ABI 4) */
+    /* Iteration-tail hand-over of the RICCATI (lane) solver (ABI 6; -1 = the default policy; the
+     * environment variables MMPC_TAIL_CAP / MMPC_TAIL_WAVE / MMPC_TAIL_ROUNDS, read at mmpc_create, override them for
+     * tests and A/B runs).  An instance still unconverged at the stop test of iteration tail_cap, or from iteration 2
+     * on once at most tail_wave_max lanes of its 64-instance wave are still iterating, continues in a 16-lane resume
+     * launch on the same stream, from the same iterate with the same algorithm.  The two kernels round differently,
+     * so an instance's bits (and, within the stop test's roundoff, its iteration count) depend on whether it was
+     * handed over -- which the wave rule decides by its wave-mates: the same instance solved alone (B = 1, the
+     * calc_u case), inside another batch or in another shard of a multi-device solve agrees to 1e-10 relative in V*
+     * (tests/test_gpu_tail.py), not bit for bit.  tail_cap = 0 turns the hand-over off: results then depend only on
+     * the instance's own data. */
+    int32_t tail_cap;      /* -1: 4 for unbounded solves, none (the wave rule alone) for bounded ones; 0: off */
+    int32_t tail_wave_max; /* -1: 8 lanes (unbounded), 4 (bounded); 0: no wave rule; <= 64 */
+    int32_t tail_rounds;   /* resume slots in rounds of up to 4 one-wave workgroups per CU; -1: 4 */
 } mmpc_opts;
 
 typedef struct mmpc_model_info {
@@ -285,7 +297,9 @@ int mmpc_multi_num_devices(const mmpc_multi* m, int32_t* n);
 int mmpc_multi_handle(mmpc_multi* m, int32_t g, mmpc_handle** h);
 /* mmpc_solve_batch_host contract for the whole batch: shard g = mmpc_shard(B, n_devices, g) is solved on device g
  * (H2D, solve, D2H on that device's stream, all devices concurrently) straight from/into the caller's arrays;
- * synchronous.  Results equal a single-device solve of the same instances bit for bit. */
+ * synchronous.  Results equal a single-device solve of each shard bit for bit; against a single-device solve of the
+ * whole batch they are bit for bit except where the RICCATI solver's iteration-tail hand-over decides differently
+ * for a different wave composition (opts.tail_cap: 1e-10 relative in V*, tests/test_gpu_multi.py). */
 int mmpc_multi_solve_batch_host(mmpc_multi* m, int64_t B, const double* x0, const double* u_prev,
                                 const double* traj, const double* weights, int64_t weights_stride,
                                 const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,
@@ -301,7 +315,8 @@ int mmpc_multi_solve_batch_host(mmpc_multi* m, int64_t B, const double* x0, cons
  * stream): the call's first RCCL operation is ordered after the work already queued there, and work queued there
  * later sees the results.  Per-instance weights (weights_stride >= nx + 2 nu) need (B - 1) weights_stride + nx + 2 nu
  * doubles.  Every RCCL operation's result is checked; after an error every stream of the call is drained before the
- * call returns.  Synchronous; results equal a single-device solve bit for bit. */
+ * call returns.  Synchronous; results as mmpc_multi_solve_batch_host's.  `stream` must belong to the first device
+ * (MMPC_ERR_INVALID_ARG otherwise). */
 int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, const double* u_prev,
                                 const double* traj, const double* weights, int64_t weights_stride,
                                 const double* u_lb, const double* u_ub, double* V_inout, int32_t* status,

@@ -12,8 +12,9 @@
 // Accuracy: |x| <= 2^20 pi/2: within 1 ulp of libm (absolute error <= 1.2e-16) in tests/test_fast_trig.py (random
 // arguments up to 1.6e6 and the multiples of pi/2 up to 1e5 pi/2).  Beyond that the reduction would lose bits: the
 // device build returns NaN there (only a diverging iterate gets that far; the solver then reports the instance
-// non-finite), the host build switches to libm.  The quadrant is formed without an out-of-range int conversion for
-// every x.  NaN and +-inf give NaN, as the device library.
+// non-finite; the oracle applies the same domain to its model evaluations, oracle/mmpc_oracle.c kTrigDomain), the host
+// build switches to libm (NaN and inf too, so the host never converts a NaN quadrant to int).  The quadrant is formed
+// without an out-of-range int conversion for every finite x.  NaN and +-inf give NaN, as the device library.
 #pragma once
 #include <math.h>
 
@@ -55,7 +56,7 @@ inline trig_cptr trig_table() { return kTrigConst; }
 // s = sin x, c = cos x; K = trig_table() (one table pointer may serve several calls of one evaluation)
 MMPC_TRIG_FN void sincos_fast(trig_cptr K, double x, double* s, double* c) {
 #if !defined(__HIPCC__) && !defined(MMPC_TRIG_DEVICE_PATH_ON_HOST)
-    if (fabs(x) > 1647099.3291652855) {   // 2^20 pi/2: beyond it the host build (checks, oracle helpers) uses libm
+    if (!(fabs(x) <= 1647099.3291652855)) {   // beyond 2^20 pi/2, and NaN / inf: the host build (checks) uses libm
         *s = sin(x);
         *c = cos(x);
         return;

@@ -15,6 +15,7 @@ hipError_t launch_group_two_link(bool exact, dim3 grid, dim3 block, size_t lds, 
 hipError_t launch_group_two_link_bounded(bool xb, bool exact, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
                                          const SolveParams& p, const GroupWork& gwk);
 // the phase-timing tables of those units (diagnostic build; mmpc_debug_phase_cycles adds them to its own)
-hipError_t group_two_link_phase_cycles(unsigned long long* out16, bool reset);
-hipError_t group_two_link_bounded_phase_cycles(unsigned long long* out16, bool reset);
+// (the first n <= kPhaseSlots slots of the unit's table)
+hipError_t group_two_link_phase_cycles(unsigned long long* out16, int n, bool reset);
+hipError_t group_two_link_bounded_phase_cycles(unsigned long long* out16, int n, bool reset);
 }  // namespace mmpc

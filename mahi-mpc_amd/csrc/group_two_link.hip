@@ -27,10 +27,10 @@ hipError_t launch(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const S
     return hipGetLastError();
 }
 // this translation unit's copy of the phase-timing table (as lane_kernels.hip)
-hipError_t unit_phase_cycles(unsigned long long* out16, bool reset) {
-    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mmpc_phase_cycles), 16 * sizeof(unsigned long long));
+hipError_t unit_phase_cycles(unsigned long long* out16, int n, bool reset) {
+    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mmpc_phase_cycles), n * sizeof(unsigned long long));
     if (e == hipSuccess && reset) {
-        unsigned long long z[16] = {0};
+        static const unsigned long long z[kPhaseSlots] = {0};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z));
     }
     return e;
@@ -43,7 +43,9 @@ hipError_t launch_group_two_link(bool exact, dim3 grid, dim3 block, size_t lds, 
     return exact ? launch<false, false, true>(grid, block, lds, stream, p, gwk)
                  : launch<false>(grid, block, lds, stream, p, gwk);
 }
-hipError_t group_two_link_phase_cycles(unsigned long long* out16, bool reset) { return unit_phase_cycles(out16, reset); }
+hipError_t group_two_link_phase_cycles(unsigned long long* out16, int n, bool reset) {
+    return unit_phase_cycles(out16, n, reset);
+}
 #else
 hipError_t launch_group_two_link_bounded(bool xb, bool exact, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
                                          const SolveParams& p, const GroupWork& gwk) {
@@ -51,8 +53,8 @@ hipError_t launch_group_two_link_bounded(bool xb, bool exact, dim3 grid, dim3 bl
     return exact ? launch<true, false, true>(grid, block, lds, stream, p, gwk)
                  : launch<true>(grid, block, lds, stream, p, gwk);
 }
-hipError_t group_two_link_bounded_phase_cycles(unsigned long long* out16, bool reset) {
-    return unit_phase_cycles(out16, reset);
+hipError_t group_two_link_bounded_phase_cycles(unsigned long long* out16, int n, bool reset) {
+    return unit_phase_cycles(out16, n, reset);
 }
 #endif
 }  // namespace mmpc

@@ -14,5 +14,5 @@ struct LaneWork;
 int launch_lane_kernels(int model_id, bool fp32, bool bounded, bool xb, bool exact, dim3 grid, dim3 block,
                         hipStream_t stream, const SolveParams& p, const LaneWork& lw);
 // the phase-timing table of the lane kernels (diagnostic build; mmpc_debug_phase_cycles adds it to its own)
-hipError_t lane_phase_cycles(unsigned long long* out16, bool reset);
+hipError_t lane_phase_cycles(unsigned long long* out16, int n, bool reset);
 }  // namespace mmpc

@@ -79,9 +79,9 @@ struct mmpc_handle {
     int ws_dev = -1;
     // iteration-tail hand-over: cap override from MMPC_TAIL_CAP at creation (-1: the default policy),
     // compute units of the device (slots of the resume launch)
-    int tail_cap_env = -1;
-    int tail_wave_env = -1;    // MMPC_TAIL_WAVE: hand over when at most this many lanes of a wave are left (-1: 8)
-    int tail_rounds_env = -1;   // MMPC_TAIL_ROUNDS: rounds of resume workgroups (-1: 4)
+    int tail_cap_env = -1;      // MMPC_TAIL_CAP (test / A/B override of opts.tail_cap; -1: not set)
+    int tail_wave_env = -1;     // MMPC_TAIL_WAVE (override of opts.tail_wave_max)
+    int tail_rounds_env = -1;   // MMPC_TAIL_ROUNDS (override of opts.tail_rounds)
     int cu_count = 0;
     // state bounds of x_1..x_N (JSON x_min/x_max, or mmpc_set_state_bounds); copied into each launch's arguments
     double x_lb[16], x_ub[16];
@@ -212,6 +212,11 @@ int validate_opts(const mmpc_opts* o) {
         return fail(MMPC_ERR_INVALID_ARG, "unknown init_states");
     if (o->hessian < MMPC_HESSIAN_AUTO || o->hessian > MMPC_HESSIAN_EXACT)
         return fail(MMPC_ERR_INVALID_ARG, "unknown hessian");
+    if (o->tail_cap < -1 || o->tail_cap >= 1000) return fail(MMPC_ERR_INVALID_ARG, "tail_cap must be -1 .. 999");
+    if (o->tail_wave_max < -1 || o->tail_wave_max > 64)
+        return fail(MMPC_ERR_INVALID_ARG, "tail_wave_max must be -1 .. 64");
+    if (o->tail_rounds < -1 || o->tail_rounds == 0 || o->tail_rounds >= 1000)
+        return fail(MMPC_ERR_INVALID_ARG, "tail_rounds must be -1 or 1 .. 999");
     return MMPC_OK;
 }
 
@@ -483,7 +488,11 @@ __device__ __forceinline__ double affine_draw(double lo, double span, double u) 
 // series, strided stores, 16 CUs busy at cfg#2: 12.3 us per batch); a first round-5 version redrew every instance's
 // parameters in each stage's thread (5.2 us at cfg#2 but 165 us at cfg#3: the 64-bit multiplies of splitmix64).
 // The phase argument is formed without FMA contraction, as the C oracle.
+// Round 6: the block's target rows (I N nx doubles, contiguous in traj) are staged in LDS and written out with
+// consecutive lanes on consecutive doubles: one thread per stage wrote its row with nx stores of 8 bytes at a 64-byte
+// lane stride (8 cache-line segments per store instruction; 131 us per cfg#3 batch).  N <= 256 always fits (I N <= 256).
 constexpr int kSynthThreads = 256;
+constexpr int kSynthStaged = 2048;   // doubles of LDS for the staged rows
 
 // cfg#2: q ~ U[-pi/4, pi/4], qdot ~ U[-1, 1], u_prev ~ U[-5, 5]; a ~ U[0.5, 1], f ~ U[0.25, 1] Hz, phase ~ U[0, 2 pi];
 // r_k = [a sin(2 pi f t_k + phase), -a sin(.), 2 pi f a cos(.), -2 pi f a cos(.)], t_k = k h
@@ -508,6 +517,8 @@ __global__ __launch_bounds__(kSynthThreads) void synth_two_link_kernel(uint64_t 
         else dr[i][2] = affine_draw(0.0, 2.0 * PI, u);
     }
     __syncthreads();
+    __shared__ double so[kSynthStaged];
+    const bool staged = I * N * 4 <= kSynthStaged;
     for (int t = threadIdx.x; t < I * N; t += kSynthThreads) {
         const int i = t / N, k = t - i * N;
         const int64_t b = b0 + i;
@@ -522,11 +533,17 @@ __global__ __launch_bounds__(kSynthThreads) void synth_two_link_kernel(uint64_t 
         double sn, cn;
         sincos(arg, &sn, &cn);   // one argument reduction for both (the device library's sin and cos values)
         const double sv = a * sn, cv = cs * cn;
-        double* r = traj + (b * N + k) * 4;
+        double* r = staged ? so + t * 4 : traj + (b * N + k) * 4;
         r[0] = sv;
         r[1] = -sv;
         r[2] = cv;
         r[3] = -cv;
+    }
+    if (staged) {   // the block's rows are contiguous in traj: coalesced copy-out
+        __syncthreads();
+        const int64_t nb = B - b0 < I ? B - b0 : I;
+        double* const dst = traj + b0 * N * 4;
+        for (int t = threadIdx.x; t < nb * N * 4; t += kSynthThreads) dst[t] = so[t];
     }
 }
 
@@ -555,11 +572,13 @@ __global__ __launch_bounds__(kSynthThreads) void synth_exo_kernel(uint64_t seed,
         else dr[i][j - 12] = affine_draw(0.0, 2.0 * PI, u);
     }
     __syncthreads();
+    __shared__ double so[kSynthStaged];
+    const bool staged = I * N * 8 <= kSynthStaged;
     for (int t = threadIdx.x; t < I * N; t += kSynthThreads) {
         const int i = t / N, k = t - i * N;
         const int64_t b = b0 + i;
         if (b >= B) continue;
-        double* r = traj + (b * N + k) * 8;
+        double* r = staged ? so + t * 8 : traj + (b * N + k) * 8;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const double a = dr[i][j], f = dr[i][4 + j], ph = dr[i][8 + j];
@@ -574,6 +593,12 @@ __global__ __launch_bounds__(kSynthThreads) void synth_exo_kernel(uint64_t seed,
             r[j] = a * sn;
             r[4 + j] = cs * cn;
         }
+    }
+    if (staged) {   // the block's rows are contiguous in traj: coalesced copy-out
+        __syncthreads();
+        const int64_t nb = B - b0 < I ? B - b0 : I;
+        double* const dst = traj + b0 * N * 8;
+        for (int t = threadIdx.x; t < nb * N * 8; t += kSynthThreads) dst[t] = so[t];
     }
 }
 
@@ -778,13 +803,17 @@ TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded, int
     // bounded solves (state: interior point; control: projected SQP with its QP re-solves) hand over by the wave rule
     // alone: their counts spread (exo |u| <= 0.5: 4.3 mean, 12 max), and a cap either hands over too many or none
     const bool spread = xb || bounded;
-    const int cap = h->tail_cap_env >= 0 ? h->tail_cap_env : (spread ? kNoCap : 4);
+    // opts.tail_* (ABI 6), the MMPC_TAIL_* environment overriding them (A/B and tests); -1: the default policy
+    const int cap_o = h->tail_cap_env >= 0 ? h->tail_cap_env : h->opts.tail_cap;
+    const int wave_o = h->tail_wave_env >= 0 ? h->tail_wave_env : h->opts.tail_wave_max;
+    const int rounds_o = h->tail_rounds_env > 0 ? h->tail_rounds_env : h->opts.tail_rounds;
+    const int cap = cap_o >= 0 ? cap_o : (spread ? kNoCap : 4);
     if (cap <= 0 || (cap >= p.max_iter && !spread)) return t;
     // wave rule threshold: 8 lanes (unbounded: only the thin tails of loose tolerances use it), 4 for bounded solves,
     // whose handed-over instances need several more iterations (exo at cfg#3 size, ms without / with 4: |qdot| <= 1.5
     // 65.3 / 60.5 (1 / 2 / 3 / 6 lanes: 62.2 / 61.0 / 61.0 / 67.6, profiles/r05/xbwave); |u| <= 0.5 36.9 / 30.1, |u| <= 2
     // 22.7 / 22.2 (8 lanes: 38.4 / 21.0; caps 4-8 beside it, profiles/r05/ubsweep))
-    const int wave_max = h->tail_wave_env >= 0 ? h->tail_wave_env : (spread ? 4 : 8);
+    const int wave_max = wave_o >= 0 ? wave_o : (spread ? 4 : 8);
     if (spread && cap >= p.max_iter && wave_max <= 0) return t;
     const size_t inst = static_cast<size_t>(group_lds_doubles(mi.num_x, mi.num_u, h->nq, mi.num_shooting_nodes,
                                                               bounded && !xb, false, xb)) * sizeof(double);
@@ -796,7 +825,7 @@ TailPlan tail_plan(const mmpc_handle* h, const SolveParams& p, bool bounded, int
     t.gpw = gpw;
     t.lds = gpw * inst;
     // up to four rounds of resume workgroups (slots nobody claimed exit at once, so spare slots cost nothing)
-    const int rounds = h->tail_rounds_env > 0 ? h->tail_rounds_env : 4;
+    const int rounds = rounds_o > 0 ? rounds_o : 4;
     t.slots = static_cast<int>(std::min<int64_t>({p.B, kTailMaxSlots, (int64_t)rounds * per_cu * cu * gpw}));
     if (xb)
         t.xb_ws_bytes = static_cast<size_t>(group_ws_doubles(mi.num_x, mi.num_u, mi.num_shooting_nodes, false, true)) *
@@ -1048,6 +1077,9 @@ void mmpc_default_opts(mmpc_opts* o) {
     o->factor_fp32 = 0;
     o->init_states = MMPC_INIT_AS_GIVEN;
     o->hessian = MMPC_HESSIAN_AUTO;
+    o->tail_cap = -1;   // the iteration-tail hand-over's default policy
+    o->tail_wave_max = -1;
+    o->tail_rounds = -1;
 }
 
 int mmpc_create_from_json(const char* json_text, const mmpc_opts* opts, mmpc_handle** out) {
@@ -1156,16 +1188,18 @@ int mmpc_get_state_bounds(const mmpc_handle* h, double* x_lb, double* x_ub) {
 int mmpc_reserve_workspace(mmpc_handle* h, int64_t B, uint64_t* bytes) {
     if (!h) return fail(MMPC_ERR_INVALID_ARG, "null handle");
     if (B < 0) return fail(MMPC_ERR_INVALID_ARG, "B < 0");
-    // + the tail hand-over list (+ a state-bounded solve's resume workspace, sized by the device's CUs: 256 until
-    // a device was queried)
+    // + the tail hand-over list + a state-bounded solve's resume workspace (sized by the device's CUs: 256 until a
+    // device was queried), reserved whether or not the handle has state bounds now: a later mmpc_set_state_bounds must
+    // not make a solve grow the workspace (a hipFree / hipMalloc inside a stream-ordered solve, or under a captured
+    // hipGraph that still points at the old buffer)
     auto total = [&]() {
         SolveParams p{};
         p.B = B;
         p.max_iter = h->opts.max_iter;
-        p.x_bounded = h->x_bounded;
+        p.x_bounded = 1;
         p.is_linear = h->info.is_linear;
         const int cu = h->cu_count > 0 ? h->cu_count : 256;
-        return solver_workspace_bytes(h, B) + kTailBytes + (h->x_bounded ? tail_plan(h, p, false, cu).xb_ws_bytes : 0);
+        return solver_workspace_bytes(h, B) + kTailBytes + tail_plan(h, p, false, cu).xb_ws_bytes;
     };
     if (bytes) *bytes = B == 0 ? 0 : total();
     if (B == 0) return MMPC_OK;
@@ -1696,6 +1730,13 @@ int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, cons
     // the caller's inputs on the first device are complete before RCCL reads them: the first device's stream waits
     // for the caller's stream (no device-wide synchronisation); at the end the caller's stream waits for the results
     hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
+    if (caller) {   // the bridges below record on and wait with the caller's stream from the first device
+        hipDevice_t sd = -1;
+        MMPC_HIP(hipStreamGetDevice(caller, &sd));
+        if (sd != m->dev[0])
+            return fail(MMPC_ERR_INVALID_ARG, "stream belongs to device " + std::to_string(sd) +
+                                                  ", not to the multi handle's first device " + std::to_string(m->dev[0]));
+    }
     {
         DeviceGuard dg(m->dev[0]);
         hipEvent_t ev;
@@ -1794,8 +1835,9 @@ int mmpc_multi_solve_batch_rccl(mmpc_multi* m, int64_t B, const double* x0, cons
     {   // later work on the caller's stream sees the gathered results
         DeviceGuard dg(m->dev[0]);
         hipEvent_t ev;
-        MMPC_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        hipError_t e = hipEventRecord(ev, m->st[0]);
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return drain(fail(MMPC_ERR_HIP, std::string("event: ") + hipGetErrorString(e)));
+        e = hipEventRecord(ev, m->st[0]);
         if (e == hipSuccess) e = hipStreamWaitEvent(caller, ev, 0);
         (void)hipEventDestroy(ev);
         if (e != hipSuccess) return drain(fail(MMPC_ERR_HIP, std::string("event: ") + hipGetErrorString(e)));
@@ -1823,28 +1865,31 @@ const char* mmpc_last_error(void) { return g_last_error.c_str(); }
 
 // Internal diagnostic: per-phase s_memtime cycle totals of the SQP kernel (all zero unless the library
 // was built with -DMMPC_PHASE_TIMING, i.e. lib/libmmpc_timing.so).  out[15] = number of waves.
-// sums, except slots 10-12 (latest end, ~earliest start, longest wave: sqp_wave.h MMPC_PHASE_FLUSH), which are maxima
-static void merge_phase_tables(unsigned long long* out16, const unsigned long long* t) {
-    for (int i = 0; i < 16; ++i) out16[i] = (i >= 10 && i <= 12) ? std::max(out16[i], t[i]) : out16[i] + t[i];
+// sums, except slots 10-12 (latest end, ~earliest start, longest wave: sqp_wave.h MMPC_PHASE_FLUSH), which are maxima;
+// the per-wave slots 16.. are written by one unit only per launch (the others hold zeros after a reset)
+static void merge_phase_tables(unsigned long long* out, const unsigned long long* t, int n) {
+    for (int i = 0; i < n; ++i) out[i] = (i >= 10 && i <= 12) ? std::max(out[i], t[i]) : out[i] + t[i];
 }
-int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) {
-    if (!out16) return fail(MMPC_ERR_INVALID_ARG, "null");
-    MMPC_HIP(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mmpc_phase_cycles), 16 * sizeof(unsigned long long)));
+// the first n (<= kPhaseSlots) slots of the merged tables of every translation unit
+int mmpc_debug_phase_table(unsigned long long* out, int n, int reset) {
+    if (!out || n < 16 || n > kPhaseSlots) return fail(MMPC_ERR_INVALID_ARG, "null or n out of 16 .. kPhaseSlots");
+    MMPC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mmpc_phase_cycles), n * sizeof(unsigned long long)));
     if (reset) {
-        unsigned long long z[16] = {0};
+        static const unsigned long long z[kPhaseSlots] = {0};
         MMPC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z)));
     }
-    unsigned long long lane[16];   // the lane kernels' table lives in their own translation unit (lane_launch.h)
-    MMPC_HIP(lane_phase_cycles(lane, reset != 0));
-    merge_phase_tables(out16, lane);
+    std::vector<unsigned long long> t(static_cast<size_t>(n));
+    MMPC_HIP(lane_phase_cycles(t.data(), n, reset != 0));   // the lane kernels' unit (lane_launch.h)
+    merge_phase_tables(out, t.data(), n);
 #if MMPC_BUILTIN_MODELS
-    MMPC_HIP(group_two_link_phase_cycles(lane, reset != 0));   // the 2-link group kernels' units (group_launch.h)
-    merge_phase_tables(out16, lane);
-    MMPC_HIP(group_two_link_bounded_phase_cycles(lane, reset != 0));
-    merge_phase_tables(out16, lane);
+    MMPC_HIP(group_two_link_phase_cycles(t.data(), n, reset != 0));   // the 2-link group kernels' units (group_launch.h)
+    merge_phase_tables(out, t.data(), n);
+    MMPC_HIP(group_two_link_bounded_phase_cycles(t.data(), n, reset != 0));
+    merge_phase_tables(out, t.data(), n);
 #endif
     return MMPC_OK;
 }
+int mmpc_debug_phase_cycles(unsigned long long* out16, int reset) { return mmpc_debug_phase_table(out16, 16, reset); }
 
 // Internal diagnostic (not part of include/mmpc.h): the handle's Riccati workspace (device pointer and size), e.g. to
 // read the gains [K_k | kff_k] a solve left there (tools/xb_diag.py)

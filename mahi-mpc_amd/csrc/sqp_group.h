@@ -1492,6 +1492,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             // the stores of the other lanes of this wave must be visible to the sweep's loads
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            MMPC_PHASE(9);   // (timing build: "check" = the stop test and this W pass)
         }
         // exact Hessian in this iteration's QP solves (false after a Gauss-Newton fallback)
         bool use_w = EXACT;

@@ -289,7 +289,15 @@ __device__ __forceinline__ double rcp_nr(double a) {
 // ---------------- diagnostic phase timing (separate build, -DMMPC_PHASE_TIMING) ----------------
 // s_memtime stamps between phases, accumulated per wave and added to a device table at exit.
 // Only the diagnostic library libmmpc_timing.so is built with it; its run time is not quoted.
-__device__ unsigned long long g_mmpc_phase_cycles[16];
+// slots 16..16+4095 (round 6): each wave's wall-clock duration (s_memrealtime ticks) at 16 + blockIdx.x (one wave
+// per block in the lane and 16-lane kernels), and at 16 + 4096 + blockIdx.x its shader cycles (s_memtime) over the
+// same extent; read by mmpc_debug_phase_table
+// and, for the first 1024 waves, the ten phase sums of lanes 0, 16, 32, 48 (the first lanes of the 16-lane kernel's
+// four instance groups) at 16 + 2 * 4096 + 40 * blockIdx.x + 10 * (lane / 16)
+constexpr int kPhaseWaveLog = 4096;
+constexpr int kPhaseWavePhases = 1024;
+constexpr int kPhaseSlots = 16 + 2 * kPhaseWaveLog + 40 * kPhaseWavePhases;
+__device__ unsigned long long g_mmpc_phase_cycles[kPhaseSlots];
 #ifdef MMPC_PHASE_TIMING
 // Slots 10-14 (round 6): the wave's wall-clock extent from s_memrealtime (100 MHz) -- 10: latest end, 11: ~earliest
 // start (atomicMax of the complement), 12: longest wave, 13: sum of wave durations, 14: sum of shader cycles (s_memtime)
@@ -316,6 +324,14 @@ __device__ unsigned long long g_mmpc_phase_cycles[16];
         atomicAdd(&g_mmpc_phase_cycles[13], r1_ - ph_r0);                                  \
         atomicAdd(&g_mmpc_phase_cycles[14], m1_ - ph_m0);                                  \
         atomicAdd(&g_mmpc_phase_cycles[15], 1ull);                                         \
+        if (blockIdx.x < kPhaseWaveLog) {                                                  \
+            g_mmpc_phase_cycles[16 + blockIdx.x] = r1_ - ph_r0;                            \
+            g_mmpc_phase_cycles[16 + kPhaseWaveLog + blockIdx.x] = m1_ - ph_m0;            \
+        }                                                                                  \
+    }                                                                                      \
+    if ((lane0 & 15) == 0 && blockIdx.x < kPhaseWavePhases) {                              \
+        for (int q_ = 0; q_ < 10; ++q_)                                                    \
+            g_mmpc_phase_cycles[16 + 2 * kPhaseWaveLog + 40 * blockIdx.x + 10 * (lane0 >> 4) + q_] = ph_acc[q_]; \
     }
 #else
 #define MMPC_PHASE_DECL

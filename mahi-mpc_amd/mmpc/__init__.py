@@ -50,7 +50,8 @@ BUILTIN_MODELS = ("two_link_arm", "double_pendulum", "exo_arm", "exo")  # "mmpc_
 class Opts(C.Structure):
     _fields_ = [("max_iter", C.c_int32), ("device", C.c_int32), ("tol_grad", C.c_double),
                 ("tol_defect", C.c_double), ("kkt_solver", C.c_int32), ("factor_fp32", C.c_int32),
-                ("init_states", C.c_int32), ("hessian", C.c_int32)]
+                ("init_states", C.c_int32), ("hessian", C.c_int32), ("tail_cap", C.c_int32),
+                ("tail_wave_max", C.c_int32), ("tail_rounds", C.c_int32)]
 
 
 class ModelInfo(C.Structure):
@@ -244,7 +245,8 @@ class Solver:
     """One loaded model (the reference's ModelControl without the thread/bookkeeping)."""
 
     def __init__(self, model_json=None, json_text=None, max_iter=None, tol_grad=None, tol_defect=None,
-                 device=None, kkt_solver=None, factor_fp32=None, library=None, init_states=None, hessian=None):
+                 device=None, kkt_solver=None, factor_fp32=None, library=None, init_states=None, hessian=None,
+                 tail_cap=None, tail_wave_max=None, tail_rounds=None):
         self._L = L = lib(library or (model_library(model_json) if model_json is not None else None))
         o = Opts()
         L.mmpc_default_opts(C.byref(o))
@@ -256,6 +258,12 @@ class Solver:
             o.init_states = int(init_states)
         if hessian is not None:
             o.hessian = int(hessian)
+        if tail_cap is not None:      # the lane solver's iteration-tail hand-over (ABI 6; -1 = default, 0 = off)
+            o.tail_cap = int(tail_cap)
+        if tail_wave_max is not None:
+            o.tail_wave_max = int(tail_wave_max)
+        if tail_rounds is not None:
+            o.tail_rounds = int(tail_rounds)
         if max_iter is not None:
             o.max_iter = max_iter
         if tol_grad is not None:

@@ -321,12 +321,30 @@ void oracle_exo_mass(const double* q, double* M) {
     exo_mass_and_grad(q, M, dM);
 }
 
+/* Domain of the built-in models' joint angles.  The device evaluates sin / cos of them with a reduced-range routine
+ * (mahi-mpc_amd/csrc/fast_trig.h: within 1 ulp of libm for |q| <= 2^20 pi/2) that returns NaN beyond, so the solver
+ * reports an iterate with such an angle (a diverging one: 1.6e6 rad) non-finite.  The oracle applies the same domain to
+ * the model evaluations, so both report the same status there (tests/test_gpu_trig_domain.py). */
+static const double kTrigDomain = 1647099.3291652855;
+static int angles_out_of_domain(const double* x) {
+    const int nq = t_model == ORACLE_MODEL_EXO_ARM ? 4 : (t_model == ORACLE_MODEL_TWO_LINK_ARM ? 2 : 0);
+    for (int i = 0; i < nq; ++i)
+        if (!(fabs(x[i]) <= kTrigDomain) && x[i] == x[i]) return 1;   /* NaN propagates by itself */
+    return 0;
+}
 static void model_jac(const double* x, const double* u, double* A, double* B, double* xdot) {
     if (t_model == ORACLE_MODEL_EXO_ARM) oracle_exo_jac(x, u, A, B, xdot);
     else if (t_model == ORACLE_MODEL_USER) {
         double Af[ORACLE_MAX_NX * ORACLE_MAX_NX], Bf[ORACLE_MAX_NX * ORACLE_MAX_NU];
         g_user_jac(x, u, A ? A : Af, B ? B : Bf, xdot);
     } else oracle_two_link_jac(x, u, A, B, xdot);
+    if (angles_out_of_domain(x)) {
+        for (int r = 0; r < NX; ++r) {
+            xdot[r] = NAN;
+            if (A) for (int c = 0; c < NX; ++c) A[r * NX + c] = NAN;
+            if (B) for (int c = 0; c < NU; ++c) B[r * NU + c] = NAN;
+        }
+    }
 }
 
 /* W = sum_r lam_r d^2 f_r / d(x,u)^2 ((nx+nu)^2, row-major); 0 when the model has no second derivatives */

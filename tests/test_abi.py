@@ -31,12 +31,24 @@ def test_library_is_gfx950_code_object(mmpc_mod):
 
 
 def test_abi_version_and_defaults(mmpc_mod):
-    assert mmpc_mod.lib().mmpc_abi_version() == 5
+    assert mmpc_mod.lib().mmpc_abi_version() == 6
     o = mmpc_mod.default_opts()
     assert o.max_iter == 200 and o.device == -1   # ipopt.max_iter, ModelControl.cpp:55
     assert o.tol_grad == 1e-8 and o.tol_defect == 1e-10
     assert o.kkt_solver == mmpc_mod.KKT_AUTO
     assert o.hessian == mmpc_mod.HESSIAN_AUTO
+    assert (o.tail_cap, o.tail_wave_max, o.tail_rounds) == (-1, -1, -1)   # the hand-over's default policy (ABI 6)
+
+
+@pytest.mark.parametrize("field,bad", [("tail_cap", -2), ("tail_cap", 1000), ("tail_wave_max", 65),
+                                       ("tail_wave_max", -2), ("tail_rounds", 0), ("tail_rounds", -3)])
+def test_tail_opts_validated(field, bad, model_json, mmpc_mod):
+    o = mmpc_mod.default_opts()
+    setattr(o, field, bad)
+    h = C.c_void_p()
+    L = mmpc_mod.lib()
+    assert L.mmpc_create(model_json(N=30).encode(), C.byref(o), C.byref(h)) == -1   # MMPC_ERR_INVALID_ARG
+    assert field in L.mmpc_last_error().decode()
 
 
 def test_load_model_json_like_reference(model_json, mmpc_mod):
@@ -232,17 +244,19 @@ def test_rccl_is_loadable_for_the_multi_device_path(mmpc_mod):
 
 def test_reserve_workspace_bytes_include_the_tail_hand_over(tmp_path, mmpc_mod):
     """mmpc_reserve_workspace reports its size before touching a device: the solver workspace, the iteration-tail
-    hand-over list and, for state-bounded solves, the resume launch's own workspace (sized for 256 CUs
-    until a device was queried)"""
+    hand-over list and a state-bounded solve's resume workspace (sized for 256 CUs until a device was
+    queried) -- the latter whether or not the handle has state bounds yet, so that setting them after the reservation
+    never grows the workspace inside a solve (a hipFree under a captured graph)"""
     p = mmpc_mod.write_model_json(str(tmp_path / "exo.json"), "exo", 8, 4, 2000, 50, model="exo_arm")
     s = mmpc_mod.Solver(p)
     b = C.c_uint64(0)
     s._L.mmpc_reserve_workspace(s._h, 65536, C.byref(b))   # no GPU here: an error code, the size set before it
     plain = b.value
-    assert plain > 256 + 65536 * 24
+    lane_ws = 65536 * 8 * (51 + 1) * (5 * 8 + 2 * 4 + 4 * 13 + 5 * 12)   # lane_ws_doubles(8, 4, 4, 50, xb) x B x 8 B
+    assert plain > lane_ws + 256 + 65536 * 24
     s.set_state_bounds([-np.inf] * 4 + [-1.5] * 4, [np.inf] * 4 + [1.5] * 4)
     s._L.mmpc_reserve_workspace(s._h, 65536, C.byref(b))
-    assert b.value > plain and (b.value - plain) % 8 == 0
+    assert b.value == plain
     s.set_state_bounds(None, None)
     s._L.mmpc_reserve_workspace(s._h, 65536, C.byref(b))
     assert b.value == plain

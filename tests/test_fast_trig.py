@@ -98,3 +98,20 @@ def test_huge_arguments_host_build_uses_libm(lib):
     x = np.array([2.0e6, -3.3e9, 1e15, -1e200, 1e300])
     s, c = _run(lib, x)
     assert np.array_equal(s, np.array([math.sin(v) for v in x])) and np.array_equal(c, np.array([math.cos(v) for v in x]))
+
+
+@pytest.fixture(scope="module")
+def host_ubsan(tmp_path_factory):
+    """the host build (libm beyond the reduced range) under UBSan with the float-to-int check, aborting on any report"""
+    return _build(tmp_path_factory.mktemp("fast_trig_host_ubsan"),
+                  ("-fsanitize=undefined,float-cast-overflow", "-fno-sanitize-recover=all"))
+
+
+def test_nan_and_inf_take_the_libm_path_on_the_host(host_ubsan):
+    """NaN compared false against the range limit and reached the quadrant's int conversion (undefined on the
+    host); the guard is now !(|x| <= limit), so NaN and +-inf take the libm path (UBSan would abort otherwise)"""
+    x = np.array([np.nan, -np.nan, np.inf, -np.inf, 0.5, 2.0e6])
+    s, c = _run(host_ubsan, x)
+    assert np.isnan(s[:4]).all() and np.isnan(c[:4]).all()
+    assert s[4] == math.sin(0.5) or _ulps(s[4:5], np.array([math.sin(0.5)])).max() <= 1.0
+    assert s[5] == math.sin(2.0e6) and c[5] == math.cos(2.0e6)

@@ -41,3 +41,36 @@ def test_multi_device_errors(model_json, mmpc_mod):
         mmpc_mod.MultiSolver(model_json(), [])
     with pytest.raises(mmpc_mod.MmpcError):
         mmpc_mod.MultiSolver(model_json(), [0, -1])
+
+
+def test_multi_device_lane_solver_exo_ragged_shards(tmp_path, mmpc_mod, oracle):
+    """the lane (RICCATI) solver's iteration-tail hand-over makes an instance's bits depend on its 64-lane
+    wave, so ragged shards (G = 3: shard boundaries off the 64-instance waves) agree with a single-device solve of the
+    whole batch to 1e-10 relative in V* with identical iteration counts on >= 99 % -- the contract include/mmpc.h
+    states -- while each shard equals a single-handle solve of that shard bit for bit; with the hand-over off
+    (opts.tail_cap = 0) the multi-device result equals the whole-batch solve bit for bit."""
+    B, N, G = 3000, 50, 3
+    x0, up, tr = oracle.synth(20250213, 0, B, N, H, model=oracle.EXO)
+    w = np.array([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4)
+    p = mmpc_mod.write_model_json(str(tmp_path / "exo_multi.json"), "exo", 8, 4, 2000, N, model="exo_arm")
+    single = mmpc_mod.Solver(p, kkt_solver=2).solve_batch_host(x0, up, tr, w)
+    multi = mmpc_mod.MultiSolver(p, [0] * G, kkt_solver=2)
+    m = multi.solve_batch_host(x0, up, tr, w)
+    assert (m["status"] == 0).all() and (single["status"] == 0).all()
+    same = m["iters"] == single["iters"]
+    assert same.mean() >= 0.99
+    rel = np.abs(m["V"] - single["V"]).max(1) / np.abs(single["V"]).max(1)
+    assert rel[same].max() <= 1e-10
+    shard_solver = mmpc_mod.Solver(p, kkt_solver=2)
+    for g in range(G):
+        f, c = mmpc_mod.shard(B, G, g)
+        r = shard_solver.solve_batch_host(x0[f:f + c], up[f:f + c], tr[f:f + c], w)
+        np.testing.assert_array_equal(r["V"], m["V"][f:f + c])
+        np.testing.assert_array_equal(r["iters"], m["iters"][f:f + c])
+    multi.close()
+    off_single = mmpc_mod.Solver(p, kkt_solver=2, tail_cap=0).solve_batch_host(x0, up, tr, w)
+    off_multi = mmpc_mod.MultiSolver(p, [0] * G, kkt_solver=2, tail_cap=0)
+    om = off_multi.solve_batch_host(x0, up, tr, w)
+    for k in ("V", "status", "iters", "kkt"):
+        np.testing.assert_array_equal(om[k], off_single[k])
+    off_multi.close()

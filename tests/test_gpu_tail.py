@@ -184,3 +184,34 @@ def test_tail_handover_tiny_and_ragged_batches(B, mmpc_mod, oracle, tmp_path, mo
                            x_lb=xl, x_ub=xu)
     assert (r["status"] == 0).all()
     _compare(r, o)
+
+
+def test_batch_composition_single_instance_vs_full_batch(mmpc_mod, oracle, tmp_path):
+    """VERDICT r5 ask 7: the hand-over decides by an instance's wave-mates (the wave rule) and by the slots, so the same
+    instance solved alone (B = 1, ModelControl::calc_u's call, ModelControl.cpp:159) -- where from iteration 2 on it is
+    the only lane of its wave and continues in the 16-lane resume launch -- and inside the full cfg#3 batch agree to
+    1e-10 relative in V* with identical iteration counts on >= 99 % of the instances, not bit for bit (include/mmpc.h,
+    mmpc_opts.tail_cap).  With the hand-over off (opts.tail_cap = 0) every lane is independent: bit for bit."""
+    N, B = 50, 65536
+    x0, up, tr = oracle.synth(20250213, 0, B, N, H, model=oracle.EXO)
+    p = mmpc_mod.write_model_json(str(tmp_path / "exo_comp.json"), "exo", 8, 4, 2000, N, model="exo_arm")
+    full = mmpc_mod.Solver(p, kkt_solver=2, init_states=mmpc_mod.INIT_ZERO).solve_batch_host(x0, up, tr, W_EXO)
+    assert (full["status"] == 0).all()
+    pick = np.linspace(0, B - 1, 128).astype(int)
+    one = mmpc_mod.Solver(p, kkt_solver=2, init_states=mmpc_mod.INIT_ZERO)
+    alone = [one.solve_batch_host(x0[i:i + 1], up[i:i + 1], tr[i:i + 1], W_EXO) for i in pick]
+    it1 = np.array([a["iters"][0] for a in alone])
+    V1 = np.stack([a["V"][0] for a in alone])
+    assert all(a["status"][0] == 0 for a in alone)
+    same = it1 == full["iters"][pick]
+    assert same.mean() >= 0.99, (it1[~same], full["iters"][pick][~same])
+    assert _rel(V1[same], full["V"][pick][same]).max() <= 1e-10
+    assert (it1 >= 2).all()   # every single-instance solve reached the wave rule's iteration
+    # hand-over off through the options (ABI 6): the lane kernel alone, bit for bit in and out of the batch
+    off = mmpc_mod.Solver(p, kkt_solver=2, init_states=mmpc_mod.INIT_ZERO, tail_cap=0)
+    sub = np.arange(0, B, 4096)
+    offb = off.solve_batch_host(x0[:4096 * 2], up[:4096 * 2], tr[:4096 * 2], W_EXO)
+    for i in sub[:2]:
+        a = off.solve_batch_host(x0[i:i + 1], up[i:i + 1], tr[i:i + 1], W_EXO)
+        np.testing.assert_array_equal(a["V"][0], offb["V"][i])
+        assert a["iters"][0] == offb["iters"][i]

@@ -59,12 +59,14 @@ ub = None if a.u_bound is None else torch.full((nu,), a.u_bound, **f)
 it = torch.zeros(B, dtype=torch.int32, device="cuda")
 s.solve_batch(B, x0, up, tr, w, V, None, it, None, u_lb=lb, u_ub=ub)
 torch.cuda.synchronize()
-buf = (C.c_ulonglong * 16)()
-L.mmpc_debug_phase_cycles(buf, 1)
+NSLOT = 16 + 2 * 4096 + 40 * 1024
+L.mmpc_debug_phase_table.argtypes = [C.c_void_p, C.c_int, C.c_int]
+buf = (C.c_ulonglong * NSLOT)()
+L.mmpc_debug_phase_table(buf, NSLOT, 1)
 V.zero_()
 s.solve_batch(B, x0, up, tr, w, V, None, it, None, u_lb=lb, u_ub=ub)
 torch.cuda.synchronize()
-L.mmpc_debug_phase_cycles(buf, 1)
+L.mmpc_debug_phase_table(buf, NSLOT, 1)
 cyc = np.array(buf[:10], dtype=np.float64)
 waves = buf[15]
 iters = it.cpu().numpy()
@@ -82,4 +84,28 @@ out = {"config": a.config, "tol_grad": a.tol_grad, "tol_defect": a.tol_defect, "
        "mean_clock_ghz": float(buf[14] / buf[13] * 0.1) if buf[13] else None,
        "per_phase_cycles_per_wave_iteration": {n: float(c / waves / (iters.mean() + 1)) for n, c in zip(NAMES, cyc)},
        "share": {n: float(c / cyc.sum()) for n, c in zip(NAMES, cyc)}}
+# the slowest waves (slots 16 + blockIdx.x: one wave per block) and the iteration counts of their instances
+ipw = 4 if ksolver == 3 else 64
+nw = (B + ipw - 1) // ipw   # the solve kernel's waves (a lane-kernel solve's resume launch reuses the low slots)
+dur = np.array(buf[16:16 + min(nw, 4096)], dtype=np.float64) / 100.0
+cyc_w = np.array(buf[16 + 4096:16 + 4096 + min(nw, 4096)], dtype=np.float64)
+if len(dur) and int(waves) == nw:
+    ghz = cyc_w / np.maximum(dur, 1e-9) * 1e-3
+    wm = np.pad(iters, (0, nw * ipw - B)).reshape(-1, ipw).max(1)[: len(dur)]
+    out["wave_clock_ghz_percentiles"] = {str(q): float(np.percentile(ghz, q)) for q in (0, 10, 50, 90, 100)}
+    order = np.argsort(dur)[::-1][:12]
+    out["wave_us_percentiles"] = {str(q): float(np.percentile(dur, q)) for q in (0, 10, 50, 90, 99, 100)}
+    wph4 = np.array(buf[16 + 2 * 4096:16 + 2 * 4096 + 40 * 1024], dtype=np.float64).reshape(1024, 4, 10)
+    wph = wph4[:, 0]   # lane 0
+    if len(dur) <= 1024:   # per-phase cycles of the waves, by their slowest instance's iteration count
+        out["phase_cycles_by_wave_max_iters"] = {
+            int(m): {n: float(v) for n, v in zip(NAMES, wph[: len(dur)][wm == m].mean(0))} for m in np.unique(wm)}
+    out["slowest_waves"] = [{"block": int(b), "us": float(dur[b]), "ghz": float(ghz[b]),
+                             "phases": ({n: float(v) for n, v in zip(NAMES, wph[b])} if b < 1024 else None),
+                             "phases_by_group": ([{n: float(v) for n, v in zip(NAMES, wph4[b, g])} for g in range(4)]
+                                                 if b < 1024 else None),
+                             "iters": [int(v) for v in iters[b * ipw:(b + 1) * ipw]][:16]} for b in order]
+    out["mean_us_by_wave_max_iters"] = {
+        int(m): [float(dur[wm == m].mean()), float(ghz[wm == m].mean()), int((wm == m).sum())]
+        for m in np.unique(wm)}
 print(json.dumps(out, indent=1))
