@@ -49,7 +49,8 @@ hipError_t group_two_link_phase_cycles(unsigned long long* out16, int n, bool re
 #else
 hipError_t launch_group_two_link_bounded(bool xb, bool exact, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
                                          const SolveParams& p, const GroupWork& gwk) {
-    if (xb) return launch<false, true>(grid, block, lds, stream, p, gwk);   // the interior point: Gauss-Newton only
+    if (xb) return exact ? launch<false, true, true>(grid, block, lds, stream, p, gwk)   // the interior point
+                         : launch<false, true>(grid, block, lds, stream, p, gwk);
     return exact ? launch<true, false, true>(grid, block, lds, stream, p, gwk)
                  : launch<true>(grid, block, lds, stream, p, gwk);
 }

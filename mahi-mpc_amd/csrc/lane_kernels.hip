@@ -22,8 +22,9 @@ template <class Model, class FT>
 void launch_lane(bool bounded, bool xb, bool exact, dim3 grid, dim3 block, hipStream_t stream, const SolveParams& p,
                  LaneWork lw) {
     if constexpr (HasHess<Model>::value && std::is_same<FT, double>::value) {
-        if (exact && !xb) {
-            if (bounded) sqp_lane_kernel<Model, double, true, false, true><<<grid, block, 0, stream>>>(p, lw);
+        if (exact) {
+            if (xb) sqp_lane_kernel<Model, double, false, true, true><<<grid, block, 0, stream>>>(p, lw);
+            else if (bounded) sqp_lane_kernel<Model, double, true, false, true><<<grid, block, 0, stream>>>(p, lw);
             else sqp_lane_kernel<Model, double, false, false, true><<<grid, block, 0, stream>>>(p, lw);
             return;
         }

@@ -724,17 +724,18 @@ int resolve_hessian(const mmpc_handle* h, int solver, bool u_bounded) {
     // (0.77 vs 0.91 ms: the exact solves take fewer iterations, but every re-solve after a hold repeats the costlier
     // exact Riccati sweep).  The lane kernel (round 4) takes EXACT on request; AUTO there stays
     // Gauss-Newton (its backward sweep evaluates the model's Hessian per stage).
-    const bool common = !h->x_bounded && !h->info.is_linear && !h->opts.factor_fp32;
+    // state bounds (round 6): EXACT on request (IPOPT's exact Hessian under the barrier, ModelGenerator.cpp:232,238);
+    // AUTO keeps Gauss-Newton for state-bounded solves like for control-bounded ones
+    const bool common = !h->info.is_linear && !h->opts.factor_fp32;
     const bool group_ok = common && group_capable && solver == MMPC_KKT_RICCATI_GROUP;
     const bool lane_ok = common && lane_capable && solver == MMPC_KKT_RICCATI;
     if (want == MMPC_HESSIAN_EXACT) {
         if (!group_ok && !lane_ok)
             return fail(MMPC_ERR_UNSUPPORTED, "exact Hessian: needs a model with second derivatives, a Riccati "
-                                              "solver (RICCATI_GROUP or RICCATI, fp64 factor) and a nonlinear solve "
-                                              "without state bounds");
+                                              "solver (RICCATI_GROUP or RICCATI, fp64 factor) and a nonlinear solve");
         return MMPC_HESSIAN_EXACT;
     }
-    return group_ok && dflt && !u_bounded ? MMPC_HESSIAN_EXACT : MMPC_HESSIAN_GAUSS_NEWTON;
+    return group_ok && dflt && !u_bounded && !h->x_bounded ? MMPC_HESSIAN_EXACT : MMPC_HESSIAN_GAUSS_NEWTON;
 }
 
 template <class Model, bool BOUNDED, bool XB = false, bool EXACT = false>
@@ -931,8 +932,9 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
             } else {
                 if constexpr (exact_capable<M>()) {
                     if (hess == MMPC_HESSIAN_EXACT)
-                        return bounded ? launch_group<M, true, false, true>(grid, block, lds, stream, p, gwk)
-                                       : launch_group<M, false, false, true>(grid, block, lds, stream, p, gwk);
+                        return xb        ? launch_group<M, false, true, true>(grid, block, lds, stream, p, gwk)
+                               : bounded ? launch_group<M, true, false, true>(grid, block, lds, stream, p, gwk)
+                                         : launch_group<M, false, false, true>(grid, block, lds, stream, p, gwk);
                 }
                 if (xb) return launch_group<M, false, true>(grid, block, lds, stream, p, gwk);
                 return bounded ? launch_group<M, true>(grid, block, lds, stream, p, gwk)
@@ -1016,11 +1018,15 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
                     if constexpr (std::is_same<M, TwoLinkArm>::value) {
                         const bool ex = hess == MMPC_HESSIAN_EXACT;
                         const hipError_t e =
-                            (xb || ub) ? launch_group_two_link_bounded(xb, ex && !xb, rgrid, rblock, tp.lds, stream, pr, gwk)
+                            (xb || ub) ? launch_group_two_link_bounded(xb, ex, rgrid, rblock, tp.lds, stream, pr, gwk)
                                        : launch_group_two_link(ex, rgrid, rblock, tp.lds, stream, pr, gwk);
                         return e == hipSuccess ? MMPC_OK : fail(MMPC_ERR_HIP, std::string("resume launch: ") +
                                                                                   hipGetErrorString(e));
                     } else {
+                        if constexpr (exact_capable<M>()) {
+                            if (xb && hess == MMPC_HESSIAN_EXACT)
+                                return launch_group<M, false, true, true>(rgrid, rblock, tp.lds, stream, pr, gwk);
+                        }
                         if (xb) return launch_group<M, false, true>(rgrid, rblock, tp.lds, stream, pr, gwk);
                         if constexpr (exact_capable<M>()) {
                             if (hess == MMPC_HESSIAN_EXACT)

@@ -28,6 +28,16 @@ namespace mmpc {
 #ifndef MMPC_GROUP_XB_PAIRS
 #define MMPC_GROUP_XB_PAIRS 1
 #endif
+// A/B switch (round 6, diagnostic builds): the W_k and [K_k | kff_k] records go to the HBM workspace with
+// non-temporal stores (no L2 allocation) instead of plain ones
+#ifndef MMPC_GROUP_NT_STORES
+#define MMPC_GROUP_NT_STORES 0
+#endif
+template <class T>
+__device__ __forceinline__ void ws_store(T* p, T v) {
+    if constexpr (MMPC_GROUP_NT_STORES) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 constexpr int kGroupLanes = 16;
 constexpr int kGroupsPerWave = 4;
 
@@ -148,8 +158,10 @@ __device__ __forceinline__ void group_model(bool lin, const double* lFq, const d
 
 // XB: state bounds (oracle solve_one_ip), the primal-dual interior-point variant for state AND control bounds;
 // BOUNDED: control bounds only (projected GN-SQP).  At most one of them.
-// EXACT: exact Hessian of the Lagrangian (mmpc_opts.hessian; oracle ORACLE_HESS_EXACT) -- unbounded solves of
-// models with second derivatives on the lane-distributed path.
+// EXACT: exact Hessian of the Lagrangian (mmpc_opts.hessian; oracle ORACLE_HESS_EXACT) -- solves of models with
+// second derivatives on the lane-distributed path: unbounded, control-bounded (held controls fixed in the exact QP)
+// and, round 6, state-bounded (W_k joins the barrier-augmented stage blocks; oracle solve_one_ip with the exact
+// Hessian).
 template <class Model, bool BOUNDED = false, bool XB = false, bool EXACT = false>
 __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork gw) {
     static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
@@ -1029,6 +1041,10 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             // stage k; LAST = (k == 0), peeled so that the stages k >= 1 carry no k == 0 selects or branches
             auto stage = [&](int k, auto last_c, Wb& wb) {
                 constexpr bool LAST = decltype(last_c)::value;
+#if defined(MMPC_PHASE_TIMING) && defined(MMPC_PHASE_STAGES)
+                if (gl == 0 && blockIdx.x < kPhaseWavePhases && k < 32)
+                    g_mmpc_phase_cycles[kPhaseStageLog + 128 * blockIdx.x + 32 * gi + k] = __builtin_amdgcn_s_memtime();
+#endif
                 double hFq[SQ], hFqd[FD], hFu[FU], cc[NX], u[NU], um[NU], acol[NA];
 #pragma unroll
                 for (int i = 0; i < FQ; ++i) hFq[i] = sFq[k * FQ + i];
@@ -1294,7 +1310,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                 {
                     const int col = r < NS ? r : NS;
 #pragma unroll
-                    for (int a = 0; a < NU; ++a) wK[(k * NU + a) * (NS + 1) + col] = -(r < NS ? Kcol[a] : kff[a]);
+                    for (int a = 0; a < NU; ++a) ws_store(&wK[(k * NU + a) * (NS + 1) + col], -(r < NS ? Kcol[a] : kff[a]));
                 }
                 if constexpr (LAST) return;
                 // A^T P_xx A (row r) from the broadcast P_xx, p~_x = A^T mv + Q (x_k - r_{k-1})
@@ -1332,6 +1348,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                     for (int j = 0; j < NS; ++j) {
                         double v = j < NX ? fma(dgx[j], sgk, Pn[j] + qoh[j]) : rdg[j - NX];
+                        if constexpr (EXACT) {
+                            if (j < NX) v = fma(lxm, wr[j], v);   // + W_xx row r (round 6: the exact Hessian under bounds)
+                        }
 #pragma unroll
                         for (int a = 0; a < NU; ++a) v = fma(-Ytil[a], Yb[a][j], v);
                         Prow[j] = v;
@@ -1369,7 +1388,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
             // the control-bounded sweep one stage per trip (its hold logic and relaxation rows fill the registers: two
             // stages in flight spilled to scratch inside the loop)
             using F_ = std::false_type;
-            if constexpr ((BOUNDED && !MMPC_GROUP_BOUNDED_PAIRS) || (XB && !MMPC_GROUP_XB_PAIRS)) {
+            if constexpr ((BOUNDED && !MMPC_GROUP_BOUNDED_PAIRS) || (XB && (EXACT || !MMPC_GROUP_XB_PAIRS))) {
                 for (int k = N - 1; k >= 1; --k) stage(k, F_{}, w0);
                 stage(0, std::true_type{}, w0);
             } else if ((N - 1) & 1) {
@@ -1481,18 +1500,21 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                 for (int r2 = 0; r2 < NX; ++r2)
 #pragma unroll
-                    for (int j = 0; j < KZ; ++j) dst[r2 * KZ + j] = W[r2 * KZ + j];
+                    for (int j = 0; j < KZ; ++j) ws_store(&dst[r2 * KZ + j], W[r2 * KZ + j]);
                 if constexpr (!CAFF) {
 #pragma unroll
                     for (int a = 0; a < NU; ++a)
 #pragma unroll
-                        for (int b = 0; b < NU; ++b) dst[NX * KZ + a * NU + b] = W[(NX + a) * KZ + NX + b];
+                        for (int b = 0; b < NU; ++b) ws_store(&dst[NX * KZ + a * NU + b], W[(NX + a) * KZ + NX + b]);
                 }
             }
+            MMPC_PHASE(9);   // (timing build: "check" = the stop test and this W pass up to its fence)
             // the stores of the other lanes of this wave must be visible to the sweep's loads
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            MMPC_PHASE(9);   // (timing build: "check" = the stop test and this W pass)
+#ifdef MMPC_PHASE_FENCE_IN_LOAD
+            MMPC_PHASE(0);   // (diagnostic: the fence's wait for the W stores, accumulated with the load phase)
+#endif
         }
         // exact Hessian in this iteration's QP solves (false after a Gauss-Newton fallback)
         bool use_w = EXACT;

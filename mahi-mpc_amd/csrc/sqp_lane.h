@@ -197,7 +197,9 @@ __device__ __forceinline__ gmem<double>* stage_ptr(double* wsb, int64_t k, int S
 // lam_{k+1,NQ+s} d^2 acc_s / d(x_k,u_k)^2 (Model::eval_hess at the iterate, lam the adjoint of this sweep) to H_ww,
 // H_wx and the x block of P~_k; a sweep whose H_ww is not positive definite is redone without W (the Gauss-Newton
 // step).  With control bounds (BOUNDED, round 5) the held controls are fixed in the exact stage QPs exactly as in
-// the Gauss-Newton ones (the hold rule acts on H_ww, H_wx, h_w after W is added).
+// the Gauss-Newton ones (the hold rule acts on H_ww, H_wx, h_w after W is added).  With state bounds (XB, round 6:
+// IPOPT's exact Hessian under the barrier) W_k joins the barrier-augmented stage blocks (Sigma, b) -- the adjoint
+// that weights it carries the bound duals -- and a sweep whose H_ww is not positive definite is redone without W.
 template <class Model, class FT = double, bool BOUNDED = false, bool XB = false, bool EXACT = false>
 // one wave per SIMD by design (P~ in LDS, ~40 KB per wave): telling the scheduler so lets it schedule for latency
 // rather than for a second wave's registers (cfg#3: 12.06 -> 11.94 ms).  The fp32-factor variant's P~ takes 20 KB, so
@@ -208,8 +210,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(std::is_same
 sqp_lane_kernel(SolveParams p,
                                                                                                  LaneWork lw) {
     static_assert(!(BOUNDED && XB), "the interior-point variant handles the control bounds itself");
-    static_assert(!EXACT || (HasHess<Model>::value && std::is_same<FT, double>::value && !XB),
-                  "exact Hessian: fp64 solves (unbounded or control-bounded) of models with second derivatives");
+    static_assert(!EXACT || (HasHess<Model>::value && std::is_same<FT, double>::value),
+                  "exact Hessian: fp64 solves of models with second derivatives");
     constexpr int NX = Model::NX, NU = Model::NU, NQ = Model::NQ, NA = NX - NQ, NS = NX + NU, ND = NX + NU;
     constexpr int SQ = NA * NQ > 0 ? NA * NQ : 1;  // extent of the h da/dq block (empty for NQ = 0)
     static_assert(NQ >= 0 && NA >= NQ, "x = [q; z] with qdot = z[0:NQ]");

@@ -294,9 +294,12 @@ __device__ __forceinline__ double rcp_nr(double a) {
 // same extent; read by mmpc_debug_phase_table
 // and, for the first 1024 waves, the ten phase sums of lanes 0, 16, 32, 48 (the first lanes of the 16-lane kernel's
 // four instance groups) at 16 + 2 * 4096 + 40 * blockIdx.x + 10 * (lane / 16)
+// and (-DMMPC_PHASE_STAGES) the s_memtime stamp after each stage of the last Riccati sweep of each group of the first
+// 1024 waves at kPhaseStageLog + 128 * blockIdx.x + 32 * group + stage (stages < 32)
 constexpr int kPhaseWaveLog = 4096;
 constexpr int kPhaseWavePhases = 1024;
-constexpr int kPhaseSlots = 16 + 2 * kPhaseWaveLog + 40 * kPhaseWavePhases;
+constexpr int kPhaseStageLog = 16 + 2 * kPhaseWaveLog + 40 * kPhaseWavePhases;
+constexpr int kPhaseSlots = kPhaseStageLog + 128 * kPhaseWavePhases;
 __device__ unsigned long long g_mmpc_phase_cycles[kPhaseSlots];
 #ifdef MMPC_PHASE_TIMING
 // Slots 10-14 (round 6): the wave's wall-clock extent from s_memrealtime (100 MHz) -- 10: latest end, 11: ~earliest

@@ -644,6 +644,44 @@ int oracle_first_iter_filter_accepts(double J0, double c0, double Jt, double ct,
 /* projection onto [lb, ub] that keeps a NaN a NaN (fmin/fmax would replace it by a bound) */
 static double proj(double v, double lb, double ub) { return v < lb ? lb : (v > ub ? ub : v); }
 
+/* exact Hessian, condensed form (solve_one, solve_one_ip): the QP in (dx, du) gains the stage term
+ * 1/2 [dx_k; du_k]^T W_k [..] with W_k = h sum_r lam_{k+1,r} d^2 f_r/d(x_k,u_k)^2 (J/2 scale, lam = s->lam); with
+ * dx_k = Gamma_k du + d_k (S_k du = [Gamma_k du; du_k]):  H += S_k^T W_k S_k,  g += S_k^T W_k [d_k; 0]
+ * (Gamma = s->G, d = s->d). */
+static void add_exact_condensed(ws_t* s, double h) {
+    const int N = s->N, M = s->M;
+    const int K = NX + NU;
+    double W[(ORACLE_MAX_NX + ORACLE_MAX_NU) * (ORACLE_MAX_NX + ORACLE_MAX_NU)];
+    const double* T = s->G;
+    double* WS = (double*)malloc(sizeof(double) * (size_t)K * M);
+    for (int k = 0; k < N; ++k) {
+        model_hess(s->X + k * NX, s->U + k * NU, s->lam + (k + 1) * NX, W);
+        /* WS = W S_k: S_k's x rows are Gamma rows of x_k (none for k = 0), its u rows select du_k */
+        for (int i = 0; i < K; ++i)
+            for (int a = 0; a < M; ++a) {
+                double t = 0.0;
+                if (k >= 1)
+                    for (int q = 0; q < NX; ++q) t += W[i * K + q] * T[(size_t)((k - 1) * NX + q) * M + a];
+                if (a / NU == k) t += W[i * K + NX + a % NU];
+                WS[(size_t)i * M + a] = h * t;
+            }
+        for (int a = 0; a < M; ++a) {
+            /* (S^T W S)[a][b] = sum_i S[i][a] WS[i][b] ; (S^T W [d; 0])[a] = sum_i S[i][a] (W [d;0])[i] */
+            for (int i = 0; i < K; ++i) {
+                double sia;
+                if (i < NX) sia = (k >= 1) ? T[(size_t)((k - 1) * NX + i) * M + a] : 0.0;
+                else sia = (a == k * NU + (i - NX)) ? 1.0 : 0.0;
+                if (sia == 0.0) continue;
+                for (int b = 0; b < M; ++b) s->H[a * M + b] += sia * WS[(size_t)i * M + b];
+                double wd = 0.0;
+                for (int q = 0; q < NX; ++q) wd += W[i * K + q] * s->d[k * NX + q];
+                s->g[a] += sia * h * wd;
+            }
+        }
+    }
+    free(WS);
+}
+
 static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, const double* traj,
                      const double* w, const double* u_lb, const double* u_ub, int max_iter,
                      double tol_grad, double tol_defect, double* V, int32_t* iters_out,
@@ -792,36 +830,7 @@ static int solve_one(ws_t* s, double h, const double* x0, const double* u_prev, 
         if (use_exact) {
             memcpy(s->Hgn, s->H, sizeof(double) * M * M);
             memcpy(s->ggn, s->g, sizeof(double) * M);
-            const int K = NX + NU;
-            double W[(ORACLE_MAX_NX + ORACLE_MAX_NU) * (ORACLE_MAX_NX + ORACLE_MAX_NU)];
-            double* T = s->G;  /* Gamma is read below only through S; W S goes to a scratch row block */
-            double* WS = (double*)malloc(sizeof(double) * (size_t)K * M);
-            for (int k = 0; k < N; ++k) {
-                model_hess(s->X + k * NX, s->U + k * NU, s->lam + (k + 1) * NX, W);
-                /* WS = W S_k: S_k's x rows are Gamma rows of x_k (none for k = 0), its u rows select du_k */
-                for (int i = 0; i < K; ++i)
-                    for (int a = 0; a < M; ++a) {
-                        double t = 0.0;
-                        if (k >= 1)
-                            for (int q = 0; q < NX; ++q) t += W[i * K + q] * T[(size_t)((k - 1) * NX + q) * M + a];
-                        if (a / NU == k) t += W[i * K + NX + a % NU];
-                        WS[(size_t)i * M + a] = h * t;
-                    }
-                for (int a = 0; a < M; ++a) {
-                    /* (S^T W S)[a][b] = sum_i S[i][a] WS[i][b] ; (S^T W [d; 0])[a] = sum_i S[i][a] (W [d;0])[i] */
-                    for (int i = 0; i < K; ++i) {
-                        double sia;
-                        if (i < NX) sia = (k >= 1) ? T[(size_t)((k - 1) * NX + i) * M + a] : 0.0;
-                        else sia = (a == k * NU + (i - NX)) ? 1.0 : 0.0;
-                        if (sia == 0.0) continue;
-                        for (int b = 0; b < M; ++b) s->H[a * M + b] += sia * WS[(size_t)i * M + b];
-                        double wd = 0.0;
-                        for (int q = 0; q < NX; ++q) wd += W[i * K + q] * s->d[k * NX + q];
-                        s->g[a] += sia * h * wd;
-                    }
-                }
-            }
-            free(WS);
+            add_exact_condensed(s, h);
         }
         if (has_b) { memcpy(s->H0, s->H, sizeof(double) * M * M); memcpy(s->g0, s->g, sizeof(double) * M); }
         int gn_fallback = 0;
@@ -1444,14 +1453,18 @@ static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_pre
         const double mu_next = (e_mu <= IP_KAPPA_EPS * mu_b)
                                    ? fmax(IP_TOL_COMPL / 20.0, fmin(IP_KAPPA_MU * mu_b, pow(mu_b, IP_THETA_MU)))
                                    : mu_b;
-        /* adjoint (penalty weight, as solve_one) */
-        for (int r = 0; r < NX; ++r) s->lam[N * NX + r] = Q[r] * s->e[(N - 1) * NX + r];
+        /* adjoint of the barrier problem's Lagrangian (the merit's penalty weight, as solve_one, and the multipliers of
+         * the exact Hessian): lam_k = Q e_{k-1} + A_k^T lam_{k+1} + (z_u - z_l) of x_k -- the kernels' adjoint
+         * (sqp_lane.h / sqp_group.h XB; round 6: the bound duals' term, which the reduced gradient gz above carries
+         * as G^T zg_X, was left out here before) */
+        for (int r = 0; r < NX; ++r) s->lam[N * NX + r] = Q[r] * s->e[(N - 1) * NX + r] + zg[(N - 1) * NX + r];
         double lmax = 0.0;
         for (int r = 0; r < NX; ++r) if (fabs(s->lam[N * NX + r]) > lmax) lmax = fabs(s->lam[N * NX + r]);
         for (int k = N - 1; k >= 1; --k)
             for (int r = 0; r < NX; ++r) {
                 double t = Q[r] * s->e[(k - 1) * NX + r];
                 for (int p2 = 0; p2 < NX; ++p2) t += s->Ad[k * NX * NX + p2 * NX + r] * s->lam[(k + 1) * NX + p2];
+                t += zg[(k - 1) * NX + r];
                 s->lam[k * NX + r] = t;
                 if (fabs(t) > lmax) lmax = fabs(t);
             }
@@ -1464,6 +1477,22 @@ static int solve_one_ip(ws_t* s, double h, const double* x0, const double* u_pre
                 if (b != a) s->H[b * M + a] += t;
             }
             s->H[a * M + a] += sg[S + a];
+        }
+        /* exact Hessian (ORACLE_HESS_EXACT; IPOPT's default with the barrier, ModelGenerator.cpp:232,238): the
+         * barrier Newton matrix gains the condensed stage terms S_k^T W_k S_k (lam: the adjoint above); when the
+         * result is not positive definite this iteration takes the Gauss-Newton barrier step (the kernels redo
+         * their Riccati sweep without W: a stage H_ww not positive definite <=> the condensed matrix is not) */
+        if (g_hess_mode == ORACLE_HESS_EXACT && !g_lin && model_has_hess()) {
+            memcpy(s->Hgn, s->H, sizeof(double) * M * M);
+            memcpy(s->ggn, s->g, sizeof(double) * M);
+            add_exact_condensed(s, h);
+            memcpy(s->H0, s->H, sizeof(double) * M * M);
+            for (int a = 0; a < M; ++a) s->g0[a] = 0.0;
+            if (chol_solve(M, s->H0, s->g0) != 0) {   /* not positive definite: the Gauss-Newton step */
+                count_exact_fallback();
+                memcpy(s->H, s->Hgn, sizeof(double) * M * M);
+                memcpy(s->g, s->ggn, sizeof(double) * M);
+            }
         }
         /* rhs of the step for the barrier gradient bv (b of the monotone rule; the corrected b of Mehrotra's),
          * solved with the factor of Hc (factored by the first call), expanded to dx and dy */

@@ -175,9 +175,8 @@ def test_hessian_policy(tmp_path, model_json, mmpc_mod):
         m.Solver(model_json(N=30, name="bad"), hessian=7)
     s = m.Solver(model_json(N=30, name="ex"), hessian=m.HESSIAN_EXACT)
     assert s.hessian_for(4096) == m.HESSIAN_EXACT and s.hessian_for(4096, u_bounded=True) == m.HESSIAN_EXACT
-    s.set_state_bounds([-1.0] * 4, [1.0] * 4)
-    with pytest.raises(m.MmpcError):
-        s.hessian_for(4096)
+    s.set_state_bounds([-1.0] * 4, [1.0] * 4)   # round 6: EXACT honoured under state bounds (interior point)
+    assert s.hessian_for(4096) == m.HESSIAN_EXACT
 
 
 def test_invalid_opts_rejected(model_json, mmpc_mod):

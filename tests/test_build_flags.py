@@ -105,6 +105,10 @@ def test_greedy_unit_kernels_do_not_spill():
     assert kernels, md
     for name, v in kernels.items():
         assert v.get("vgpr_spill_count") == 0 and v.get("private_segment_fixed_size") == 0, (name, v)
+        # SGPR spills go to VGPR lanes (no scratch); 79 / 81 at the end of round 5.  Bounded so that an edit that
+        # pushes these kernels towards the 512-register profile of the six miscompiles (100-150 SGPR spills with VGPR
+        # spills) fails here first
+        assert v.get("sgpr_spill_count") <= 96, (name, v)
     # only the unbounded instantiations <TwoLinkArm, BOUNDED = false, XB = false, EXACT> live in the greedy unit
     assert all("TwoLinkArmELb0ELb0E" in k for k in kernels), sorted(kernels)
 
@@ -113,7 +117,9 @@ def test_bounded_two_link_group_kernels_in_the_basic_unit():
     obj = os.path.join(AMD, "build", "group_two_link_bounded.o")
     _need(obj)
     kernels = [k for k in _kernel_metadata(obj) if "sqp_group_kernel" in k]
-    assert sorted(k.split("TwoLinkArmE")[1][:9] for k in kernels) == ["Lb0ELb1EL", "Lb1ELb0EL", "Lb1ELb0EL"], kernels
+    # <BOUNDED, XB, EXACT>: state-bounded (Gauss-Newton and, round 6, exact) and control-bounded (both Hessians)
+    assert sorted(k.split("TwoLinkArmE")[1][:14] for k in kernels) == \
+        ["Lb0ELb1ELb0E", "Lb0ELb1ELb1E", "Lb1ELb0ELb0E", "Lb1ELb0ELb1E"], kernels
     r = _rules(os.path.join(AMD, "Makefile"))
     assert any("$(LANEFLAGS)" in l and "MMPC_GROUP_BOUNDED_UNIT" in l for l in r["build/group_two_link_bounded.o"])
     assert "build/group_two_link_bounded.o" in open(os.path.join(AMD, "Makefile")).read().split("OBJS :=")[1].split("\n")[0]

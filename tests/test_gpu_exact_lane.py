@@ -58,8 +58,8 @@ def test_group_exact_exo_vs_oracle(mmpc_mod, oracle, tmp_path):
 
 def test_exact_hessian_policy(mmpc_mod, tmp_path):
     """AUTO keeps Gauss-Newton for the exo (more iterations exact), on the lane kernel and for bounded
-    solves; an explicit EXACT is honoured on the lane kernel with and without control bounds (round 5), and refused
-    with the fp32 factor and with state bounds."""
+    solves; an explicit EXACT is honoured on the lane kernel with and without control bounds (round 5) and with state
+    bounds (round 6), and refused with the fp32 factor."""
     s = _solver(mmpc_mod, tmp_path, "exo_arm", 50)
     assert s.hessian_for(65536, False) == mmpc_mod.HESSIAN_GAUSS_NEWTON
     e = _solver(mmpc_mod, tmp_path, "exo_arm", 50, kkt_solver=2, hessian=mmpc_mod.HESSIAN_EXACT)
@@ -69,8 +69,8 @@ def test_exact_hessian_policy(mmpc_mod, tmp_path):
     with pytest.raises(mmpc_mod.MmpcError):
         f.hessian_for(64, False)
     e.set_state_bounds([-np.inf] * 4 + [-1.5] * 4, [np.inf] * 4 + [1.5] * 4)
-    with pytest.raises(mmpc_mod.MmpcError):
-        e.hessian_for(64, False)
+    assert e.hessian_for(64, False) == mmpc_mod.HESSIAN_EXACT
+    assert s.hessian_for(64, False) == mmpc_mod.HESSIAN_GAUSS_NEWTON
     t = _solver(mmpc_mod, tmp_path, "two_link_arm", 30, kkt_solver=2)
     assert t.hessian_for(64, False) == mmpc_mod.HESSIAN_GAUSS_NEWTON
     assert _solver(mmpc_mod, tmp_path, "two_link_arm", 30, kkt_solver=2).hessian_for(64, True) == \

@@ -152,3 +152,78 @@ def test_state_bounds_api(model_json, mmpc_mod):
     assert e.value.code == -4
     s.set_state_bounds(None, None)
     assert s.kkt_solver_for(64) == mmpc_mod.KKT_CONDENSED
+
+
+# ---- round 6: the exact Hessian under state bounds (VERDICT r5 ask 4; IPOPT runs nlp_hess_l whatever the bounds,
+#      ModelGenerator.cpp:232,238, with x bounds through v_min/v_max, ModelControl.cpp:37-50,156-157) ----
+XB_EXACT = [("two_link_arm", 30, 128, "group"), ("two_link_arm", 30, 128, "lane"), ("exo_arm", 50, 128, "lane"),
+            ("exo_arm", 20, 70, "group")]
+
+
+@pytest.mark.parametrize("model,N,B,solver", XB_EXACT)
+def test_state_bounds_exact_hessian_vs_oracle(model, N, B, solver, mmpc_mod, oracle, tmp_path):
+    """interior point + exact Hessian (W_k in the barrier-augmented stage blocks, the Gauss-Newton step when not
+    positive definite) against the oracle's solve_one_ip with ORACLE_HESS_EXACT: V* within 1e-10 where the
+    iteration counts agree; the same KKT point as the Gauss-Newton interior-point solve (1e-5); both iteration
+    histograms printed (|qdot| <= 1.5; exo |qdot| <= 0.3)"""
+    exo = model == "exo_arm"
+    nx, nu = (8, 4) if exo else (4, 2)
+    vb = 0.3 if exo else 1.5
+    xl = np.array([-INF] * (nx // 2) + [-vb] * (nx // 2))
+    xu = np.array([INF] * (nx // 2) + [vb] * (nx // 2))
+    ks = mmpc_mod.KKT_RICCATI_GROUP if solver == "group" else mmpc_mod.KKT_RICCATI
+    p = mmpc_mod.write_model_json(str(tmp_path / f"{model}_{N}.json"), model, nx, nu, 2000, N, model=model)
+    om = oracle.EXO if exo else oracle.TWO_LINK
+    x0, up, tr = oracle.synth(20250213, 0, B, N, 0.002, model=om)
+    if exo:
+        x0[:, 4:] = np.clip(x0[:, 4:], -0.25, 0.25)
+    else:
+        x0[:, 2:] = np.clip(x0[:, 2:], -1.4, 1.4)
+    w = np.array([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4) if exo else np.array(WEIGHTS_CFG)
+    res = {}
+    for hess in (mmpc_mod.HESSIAN_EXACT, mmpc_mod.HESSIAN_GAUSS_NEWTON):
+        s = mmpc_mod.Solver(p, max_iter=100, kkt_solver=ks, hessian=hess)
+        s.set_state_bounds(xl, xu)
+        assert s.kkt_solver_for(B) == ks and s.hessian_for(B) == hess
+        res[hess] = s.solve_batch_host(x0, up, tr, w)
+        s.close()
+    g = res[mmpc_mod.HESSIAN_EXACT]
+    oracle.exact_fallbacks(reset=True)
+    o = oracle.solve_batch(N, 0.002, x0, up, tr, w, x_lb=xl, x_ub=xu, max_iter=100, model=om,
+                           hessian=oracle.HESS_EXACT)
+    fb = oracle.exact_fallbacks(reset=True)
+    assert (g["status"] == 0).all() and (o["status"] == 0).all()
+    compare(g, o)
+    gn = res[mmpc_mod.HESSIAN_GAUSS_NEWTON]
+    assert (gn["status"] == 0).all()
+    # both stop where ||2 grad L|| <= 1e-8, ||c|| <= 1e-10 and 2 max s z <= 1e-8: the two interior-point paths end
+    # within the complementarity tolerance's effect of each other (3.6e-6 measured on the exo at N = 20)
+    assert (np.abs(g["V"] - gn["V"]).max(1) / np.abs(gn["V"]).max(1)).max() <= 1e-5
+    X = states(g["V"], N, nx, nu)
+    assert np.abs(X[:, :, nx // 2:]).max() <= vb + 1e-12
+    print(f"{model} N={N} {solver}: exact iterations {np.bincount(g['iters']).tolist()} (mean {g['iters'].mean():.2f}), "
+          f"Gauss-Newton {np.bincount(gn['iters']).tolist()} (mean {gn['iters'].mean():.2f}); oracle Gauss-Newton "
+          f"fallbacks {fb}")
+
+
+@pytest.mark.parametrize("solver", ["group", "lane"])
+def test_state_bounds_exact_hessian_match_scipy_golden(solver, mmpc_mod, tmp_path):
+    """the exact-Hessian interior point reaches the scipy golden KKT points (tests/golden/xbounds_golden.json): V*
+    within 1e-6 on every case (2-link and exo, 1-24 active bounds)"""
+    gold = load_golden("xbounds_golden.json")
+    ks = mmpc_mod.KKT_RICCATI_GROUP if solver == "group" else mmpc_mod.KKT_RICCATI
+    h = gold["h"]
+    for i, case in enumerate(gold["cases"]):
+        exo = case["model"] == "exo_arm"
+        nx, nu = (8, 4) if exo else (4, 2)
+        path = mmpc_mod.write_model_json(str(tmp_path / f"e{i}.json"), f"e{i}", nx, nu, int(h * 1e6), case["N"],
+                                         x_min=case["x_lb"], x_max=case["x_ub"],
+                                         model="exo_arm" if exo else "two_link_arm")
+        s = mmpc_mod.Solver(path, max_iter=200, kkt_solver=ks, hessian=mmpc_mod.HESSIAN_EXACT)
+        ul, uu = np.array(case["u_lb"]), np.array(case["u_ub"])
+        g = s.solve_batch_host(np.array(case["x0"])[None], np.array(case["u_prev"])[None],
+                               np.array(case["traj"])[None], np.array(case["weights"]),
+                               u_lb=None if np.isinf(ul).all() else ul, u_ub=None if np.isinf(uu).all() else uu)
+        assert g["status"][0] == 0, (i, g["status"], g["iters"])
+        Vg = np.array(case["V"])
+        assert np.abs(g["V"][0] - Vg).max() / np.abs(Vg).max() < 1e-6, i

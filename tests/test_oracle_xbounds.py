@@ -94,3 +94,51 @@ def test_oracle_mehrotra_rules_same_kkt_point(rule, golden, oracle):
         assert (np.abs(m["V"] - b["V"]).max(1) / np.abs(b["V"]).max(1)).max() < 1e-5
     finally:
         oracle.set_ip_rule(0)
+
+
+def test_oracle_state_bounds_exact_hessian_match_scipy(golden, oracle):
+    """VERDICT r5 ask 4: IPOPT runs CasADi's nlp_hess_l whatever the bounds (ModelGenerator.cpp:232,238; x bounds
+    through v_min/v_max, ModelControl.cpp:37-50,156-157).  The interior-point oracle with the exact Lagrangian Hessian
+    (the barrier Newton matrix + the condensed W_k terms; Gauss-Newton step when not positive definite) reaches the
+    same scipy golden KKT points as the Gauss-Newton one (V* 1e-6, J* 1e-8, the same active state bounds)."""
+    h = golden["h"]
+    try:
+        oracle.lib().oracle_set_hessian(oracle.HESS_EXACT)
+        for case in golden["cases"]:
+            model = oracle.EXO if case["model"] == "exo_arm" else oracle.TWO_LINK
+            nx, nu = oracle.DIMS[model]
+            N = case["N"]
+            args = (N, h, np.array(case["x0"])[None], np.array(case["u_prev"])[None], np.array(case["traj"])[None],
+                    np.array(case["weights"]))
+            kw = dict(u_lb=np.array(case["u_lb"]), u_ub=np.array(case["u_ub"]), x_lb=np.array(case["x_lb"]),
+                      x_ub=np.array(case["x_ub"]), max_iter=200, model=model, hessian=oracle.HESS_EXACT)
+            r = oracle.solve_batch(*args, **kw)
+            assert r["status"][0] == 0, (case["index"], r["status"], r["iters"])
+            V, Vg = r["V"][0], np.array(case["V"])
+            assert np.abs(V - Vg).max() / np.abs(Vg).max() < 1e-6, (case["index"], np.abs(V - Vg).max())
+            assert abs(r["J"][0] - case["J"]) / case["J"] < 1e-8
+            X = states(V, N, nx, nu)
+            xl, xu = np.array(case["x_lb"]), np.array(case["x_ub"])
+            Xg = states(Vg, N, nx, nu)
+            act_g = (np.abs(Xg - xl) < 1e-9) | (np.abs(Xg - xu) < 1e-9)
+            act = (np.abs(X - xl) < 1e-6) | (np.abs(X - xu) < 1e-6)
+            assert (act == act_g).all()
+    finally:
+        oracle.lib().oracle_set_hessian(oracle.HESS_GAUSS_NEWTON)
+
+
+def test_oracle_state_bounds_exact_vs_gauss_newton_iterations(oracle):
+    """Iteration histograms of the interior-point solve with both Hessians on 256 velocity-bounded cfg#2 instances
+    (|qdot| <= 1.5): the same KKT points (1e-6), every instance converged with both."""
+    N, h, B = 30, 0.002, 256
+    x0, up, tr = oracle.synth(20250213, 0, B, N, h)
+    w = np.array([10.0, 1.0, 5.0, 5.0, 5.0, 5.0, 0.01, 0.01])
+    xl, xu = np.array([-np.inf, -np.inf, -1.5, -1.5]), np.array([np.inf, np.inf, 1.5, 1.5])
+    gn = oracle.solve_batch(N, h, x0, up, tr, w, x_lb=xl, x_ub=xu)
+    oracle.exact_fallbacks(reset=True)
+    ex = oracle.solve_batch(N, h, x0, up, tr, w, x_lb=xl, x_ub=xu, hessian=oracle.HESS_EXACT)
+    assert (gn["status"] == 0).all() and (ex["status"] == 0).all()
+    rel = np.abs(gn["V"] - ex["V"]).max(1) / np.abs(gn["V"]).max(1)
+    assert rel.max() < 1e-6
+    print("GN", np.bincount(gn["iters"]), gn["iters"].mean(), "EXACT", np.bincount(ex["iters"]), ex["iters"].mean(),
+          "fallbacks", oracle.exact_fallbacks(reset=True))

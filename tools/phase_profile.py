@@ -59,7 +59,7 @@ ub = None if a.u_bound is None else torch.full((nu,), a.u_bound, **f)
 it = torch.zeros(B, dtype=torch.int32, device="cuda")
 s.solve_batch(B, x0, up, tr, w, V, None, it, None, u_lb=lb, u_ub=ub)
 torch.cuda.synchronize()
-NSLOT = 16 + 2 * 4096 + 40 * 1024
+NSLOT = 16 + 2 * 4096 + 40 * 1024 + 128 * 1024
 L.mmpc_debug_phase_table.argtypes = [C.c_void_p, C.c_int, C.c_int]
 buf = (C.c_ulonglong * NSLOT)()
 L.mmpc_debug_phase_table(buf, NSLOT, 1)
@@ -102,6 +102,10 @@ if len(dur) and int(waves) == nw:
             int(m): {n: float(v) for n, v in zip(NAMES, wph[: len(dur)][wm == m].mean(0))} for m in np.unique(wm)}
     out["slowest_waves"] = [{"block": int(b), "us": float(dur[b]), "ghz": float(ghz[b]),
                              "phases": ({n: float(v) for n, v in zip(NAMES, wph[b])} if b < 1024 else None),
+                             "riccati_stage_cycles_by_group": ([np.diff(np.array(buf[16 + 2 * 4096 + 40 * 1024 + 128 * b
+                                                                  + 32 * g:16 + 2 * 4096 + 40 * 1024 + 128 * b + 32 * g + N],
+                                                                 dtype=np.int64)[::-1]).tolist() for g in range(4)]
+                                                               if b < 1024 and N <= 32 else None),
                              "phases_by_group": ([{n: float(v) for n, v in zip(NAMES, wph4[b, g])} for g in range(4)]
                                                  if b < 1024 else None),
                              "iters": [int(v) for v in iters[b * ipw:(b + 1) * ipw]][:16]} for b in order]

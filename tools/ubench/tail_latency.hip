@@ -21,7 +21,7 @@ constexpr int kSteps = 4096;        // timed dependent loads
 
 __global__ __launch_bounds__(64) void kern(const int* chain, double* sink, long long* out, int spin_chaser,
                                            int spin_other, int cold, int* scratch, int with_store, const int* big,
-                                           int hbm) {
+                                           int hbm, int start) {
   const int b = blockIdx.x, t = threadIdx.x;
   const bool chaser = b < 8;
   double y = sink[b * 64 + t] + 1.0;
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(64) void kern(const int* chain, double* sink, long 
     int* sc = scratch + (size_t)b * kSteps * 16;
     if (hbm) {   // dependent loads at random lines of 64 MB: L2 / MALL misses
       const int* g = big + (size_t)b * kBigLines * 16;
-      long long j = idx;
+      long long j = start;   // a segment of the cycle no earlier launch walked (cold lines)
       for (int i = 0; i < kSteps; ++i) j = g[j * 16];
       idx = (int)j;
     } else if (with_store) {   // a store before every dependent load (gfx9: stores and loads share vmcnt)
@@ -78,6 +78,7 @@ int main() {
   long long* out;
   hipMalloc(&d, h.size() * sizeof(int));
   hipMalloc(&sink, (1024 * 64 + 1024 * 2048) * sizeof(double));
+  hipMemset(sink, 0, (1024 * 64 + 1024 * 2048) * sizeof(double));
   hipMalloc(&out, 8 * 3 * sizeof(long long));
   // hbm mode: a random cyclic permutation of 2^20 lines per chaser (8 x 64 MB)
   std::vector<int> hb((size_t)8 * kBigLines * 16, 0);
@@ -97,13 +98,15 @@ int main() {
   const int S = 200000;   // ~0.4 ms of FMAs at 1 wave / SIMD
   struct Mode { const char* name; int grid, spin_chaser, spin_other; };
   const Mode modes[] = {{"busy", 1024, S, 4 * S}, {"tail", 1024, S, S / 4}, {"lone", 8, S, 0},
-                        {"tailmem", 1024, S, -2000}};
+                        {"tailmem", 1024, S, -400}, {"busymem", 1024, S, -8000}};
   for (int ws = 0; ws < 3; ++ws)   // 0: loads, 1: store + load, 2: HBM loads
   for (int cold = 0; cold < (ws == 2 ? 1 : 2); ++cold) {
     for (const Mode& m : modes) {
       for (int rep = 0; rep < 3; ++rep) {
+        static int launch = 0;
+        ++launch;
         kern<<<m.grid, 64>>>(d, sink, out, m.spin_chaser, m.spin_other, cold || ws == 2, scratch, ws == 1, big,
-                             ws == 2);
+                             ws == 2, launch * 4099);
         hipDeviceSynchronize();
         long long o[24];
         hipMemcpy(o, out, sizeof(o), hipMemcpyDeviceToHost);
