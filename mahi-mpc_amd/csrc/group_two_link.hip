@@ -27,14 +27,7 @@ hipError_t launch(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const S
     return hipGetLastError();
 }
 // this translation unit's copy of the phase-timing table (as lane_kernels.hip)
-hipError_t unit_phase_cycles(unsigned long long* out16, int n, bool reset) {
-    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mmpc_phase_cycles), n * sizeof(unsigned long long));
-    if (e == hipSuccess && reset) {
-        static const unsigned long long z[kPhaseSlots] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z));
-    }
-    return e;
-}
+hipError_t unit_phase_cycles(unsigned long long* out16, int n, bool reset) { return phase_table_read(out16, n, reset); }
 }  // namespace
 
 #ifndef MMPC_GROUP_BOUNDED_UNIT

@@ -62,12 +62,5 @@ int launch_lane_kernels(int model_id, bool fp32, bool bounded, bool xb, bool exa
 }
 
 // this translation unit's copy of the phase-timing table (device variables are per code object without -fgpu-rdc)
-hipError_t lane_phase_cycles(unsigned long long* out16, int n, bool reset) {
-    hipError_t e = hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_mmpc_phase_cycles), n * sizeof(unsigned long long));
-    if (e == hipSuccess && reset) {
-        static const unsigned long long z[kPhaseSlots] = {0};
-        e = hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z));
-    }
-    return e;
-}
+hipError_t lane_phase_cycles(unsigned long long* out16, int n, bool reset) { return phase_table_read(out16, n, reset); }
 }  // namespace mmpc

@@ -920,25 +920,34 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         dim3 grid(grid1d(B, kGroupsPerWave)), block(64);
         const int hess = resolve_hessian(h, solver, bounded);
         if (hess < 0) return hess;
+#ifdef MMPC_GROUP_HOLD_EXIT
+        static int32_t* hold_ctr = nullptr;   // diagnostic A/B build only (sqp_group.h)
+        if (!hold_ctr) MMPC_HIP(hipMalloc(&hold_ctr, 256));
+        MMPC_HIP(hipMemsetAsync(hold_ctr, 0, sizeof(int32_t), stream));
+        SolveParams pg = p;
+        pg.tail_count = hold_ctr;
+#else
+        const SolveParams& pg = p;
+#endif
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;
             if constexpr (std::is_same<M, TwoLinkArm>::value) {   // the units of group_launch.h
                 const bool exact = hess == MMPC_HESSIAN_EXACT;
                 const hipError_t e =
-                    (bounded || xb) ? launch_group_two_link_bounded(xb, exact, grid, block, lds, stream, p, gwk)
-                                    : launch_group_two_link(exact, grid, block, lds, stream, p, gwk);
+                    (bounded || xb) ? launch_group_two_link_bounded(xb, exact, grid, block, lds, stream, pg, gwk)
+                                    : launch_group_two_link(exact, grid, block, lds, stream, pg, gwk);
                 return e == hipSuccess ? MMPC_OK : fail(MMPC_ERR_HIP, std::string("group kernel launch: ") +
                                                                           hipGetErrorString(e));
             } else {
                 if constexpr (exact_capable<M>()) {
                     if (hess == MMPC_HESSIAN_EXACT)
-                        return xb        ? launch_group<M, false, true, true>(grid, block, lds, stream, p, gwk)
-                               : bounded ? launch_group<M, true, false, true>(grid, block, lds, stream, p, gwk)
-                                         : launch_group<M, false, false, true>(grid, block, lds, stream, p, gwk);
+                        return xb        ? launch_group<M, false, true, true>(grid, block, lds, stream, pg, gwk)
+                               : bounded ? launch_group<M, true, false, true>(grid, block, lds, stream, pg, gwk)
+                                         : launch_group<M, false, false, true>(grid, block, lds, stream, pg, gwk);
                 }
-                if (xb) return launch_group<M, false, true>(grid, block, lds, stream, p, gwk);
-                return bounded ? launch_group<M, true>(grid, block, lds, stream, p, gwk)
-                               : launch_group<M, false>(grid, block, lds, stream, p, gwk);
+                if (xb) return launch_group<M, false, true>(grid, block, lds, stream, pg, gwk);
+                return bounded ? launch_group<M, true>(grid, block, lds, stream, pg, gwk)
+                               : launch_group<M, false>(grid, block, lds, stream, pg, gwk);
             }
         });
         if (rc) return rc;
@@ -1879,11 +1888,7 @@ static void merge_phase_tables(unsigned long long* out, const unsigned long long
 // the first n (<= kPhaseSlots) slots of the merged tables of every translation unit
 int mmpc_debug_phase_table(unsigned long long* out, int n, int reset) {
     if (!out || n < 16 || n > kPhaseSlots) return fail(MMPC_ERR_INVALID_ARG, "null or n out of 16 .. kPhaseSlots");
-    MMPC_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mmpc_phase_cycles), n * sizeof(unsigned long long)));
-    if (reset) {
-        static const unsigned long long z[kPhaseSlots] = {0};
-        MMPC_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z)));
-    }
+    MMPC_HIP(phase_table_read(out, n, reset != 0));   // this unit's table
     std::vector<unsigned long long> t(static_cast<size_t>(n));
     MMPC_HIP(lane_phase_cycles(t.data(), n, reset != 0));   // the lane kernels' unit (lane_launch.h)
     merge_phase_tables(out, t.data(), n);

@@ -30,6 +30,9 @@ namespace mmpc {
 #endif
 // A/B switch (round 6, diagnostic builds): the W_k and [K_k | kff_k] records go to the HBM workspace with
 // non-temporal stores (no L2 allocation) instead of plain ones
+#ifndef MMPC_GROUP_WB_COALESCED   // A/B switch: V written back 16 consecutive doubles per store instruction
+#define MMPC_GROUP_WB_COALESCED 0
+#endif
 #ifndef MMPC_GROUP_NT_STORES
 #define MMPC_GROUP_NT_STORES 0
 #endif
@@ -1864,6 +1867,14 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     if (!valid) return;
     // ---- write back V (reference layout), stage-parallel ----
     double* Vout = p.V + inst * (int64_t)NV;
+#if MMPC_GROUP_WB_COALESCED
+    // V element e on lane e mod 16: each store instruction writes 16 consecutive doubles of the instance's row
+    for (int e = gl; e < NV; e += G) {
+        const int k = e / ND, r = e - k * ND;
+        Vout[e] = r < NX ? sX[k * NX + r] : sU[k * NU + r - NX];
+    }
+    if (false)
+#endif
     for (int k = gl; k <= N; k += G) {
 #pragma unroll
         for (int r = 0; r < NX; ++r) Vout[k * ND + r] = sX[k * NX + r];
@@ -1880,6 +1891,17 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     }
     MMPC_PHASE(7);
     MMPC_PHASE_FLUSH
+#ifdef MMPC_GROUP_HOLD_EXIT
+    // diagnostic A/B (lib_var builds only): a finished wave stays resident, sleeping, until every wave of the launch
+    // has finished (bounded wait), so no wave of a solve runs while others of the launch have already left
+    if (!resume && p.tail_count) {
+        if (threadIdx.x == 0) atomicAdd(p.tail_count, 1);
+        for (int spins = 0; spins < 50000; ++spins) {
+            if (__hip_atomic_load(p.tail_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (int)gridDim.x) break;
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+#endif
 }
 
 }  // namespace mmpc

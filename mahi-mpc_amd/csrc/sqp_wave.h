@@ -299,8 +299,31 @@ __device__ __forceinline__ double rcp_nr(double a) {
 constexpr int kPhaseWaveLog = 4096;
 constexpr int kPhaseWavePhases = 1024;
 constexpr int kPhaseStageLog = 16 + 2 * kPhaseWaveLog + 40 * kPhaseWavePhases;
-constexpr int kPhaseSlots = kPhaseStageLog + 128 * kPhaseWavePhases;
+// slots 0..15 are accumulated by atomics into kPhaseSpread copies (one per 256-byte line, copy = blockIdx.x % 64) at
+// kPhaseSpreadBase and folded on the host (phase_table_read): 16 atomics of every wave on ONE line serialise in one L2
+// channel and stalled the memory operations of the waves still running (round 6)
+constexpr int kPhaseSpread = 64;
+constexpr int kPhaseSpreadBase = kPhaseStageLog + 128 * kPhaseWavePhases;
+constexpr int kPhaseSlots = kPhaseSpreadBase + 32 * kPhaseSpread;
 __device__ unsigned long long g_mmpc_phase_cycles[kPhaseSlots];
+// this translation unit's table (static: device variables are per code object without -fgpu-rdc), spread copies
+// folded into slots 0..15, the first n slots to out
+static inline hipError_t phase_table_read(unsigned long long* out, int n, bool reset) {
+    static unsigned long long full[kPhaseSlots];
+    hipError_t e = hipMemcpyFromSymbol(full, HIP_SYMBOL(g_mmpc_phase_cycles), sizeof(full));
+    if (e != hipSuccess) return e;
+    for (int c = 0; c < kPhaseSpread; ++c)
+        for (int q = 0; q < 16; ++q) {
+            const unsigned long long v = full[kPhaseSpreadBase + 32 * c + q];
+            full[q] = (q >= 10 && q <= 12) ? (v > full[q] ? v : full[q]) : full[q] + v;
+        }
+    for (int i = 0; i < n; ++i) out[i] = full[i];
+    if (reset) {
+        static const unsigned long long z[kPhaseSlots] = {0};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_mmpc_phase_cycles), z, sizeof(z));
+    }
+    return e;
+}
 #ifdef MMPC_PHASE_TIMING
 // Slots 10-14 (round 6): the wave's wall-clock extent from s_memrealtime (100 MHz) -- 10: latest end, 11: ~earliest
 // start (atomicMax of the complement), 12: longest wave, 13: sum of wave durations, 14: sum of shader cycles (s_memtime)
@@ -320,13 +343,14 @@ __device__ unsigned long long g_mmpc_phase_cycles[kPhaseSlots];
     if (lane0 == 0) {                                                                      \
         const unsigned long long r1_ = __builtin_amdgcn_s_memrealtime(),                   \
                                  m1_ = __builtin_amdgcn_s_memtime();                       \
-        for (int q_ = 0; q_ < 10; ++q_) atomicAdd(&g_mmpc_phase_cycles[q_], ph_acc[q_]);   \
-        atomicMax(&g_mmpc_phase_cycles[10], r1_);                                          \
-        atomicMax(&g_mmpc_phase_cycles[11], ~ph_r0);                                       \
-        atomicMax(&g_mmpc_phase_cycles[12], r1_ - ph_r0);                                  \
-        atomicAdd(&g_mmpc_phase_cycles[13], r1_ - ph_r0);                                  \
-        atomicAdd(&g_mmpc_phase_cycles[14], m1_ - ph_m0);                                  \
-        atomicAdd(&g_mmpc_phase_cycles[15], 1ull);                                         \
+        unsigned long long* const pc_ = g_mmpc_phase_cycles + kPhaseSpreadBase + 32 * (blockIdx.x % kPhaseSpread); \
+        for (int q_ = 0; q_ < 10; ++q_) atomicAdd(&pc_[q_], ph_acc[q_]);                   \
+        atomicMax(&pc_[10], r1_);                                                          \
+        atomicMax(&pc_[11], ~ph_r0);                                                       \
+        atomicMax(&pc_[12], r1_ - ph_r0);                                                  \
+        atomicAdd(&pc_[13], r1_ - ph_r0);                                                  \
+        atomicAdd(&pc_[14], m1_ - ph_m0);                                                  \
+        atomicAdd(&pc_[15], 1ull);                                                         \
         if (blockIdx.x < kPhaseWaveLog) {                                                  \
             g_mmpc_phase_cycles[16 + blockIdx.x] = r1_ - ph_r0;                            \
             g_mmpc_phase_cycles[16 + kPhaseWaveLog + blockIdx.x] = m1_ - ph_m0;            \

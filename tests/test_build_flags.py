@@ -118,7 +118,7 @@ def test_bounded_two_link_group_kernels_in_the_basic_unit():
     _need(obj)
     kernels = [k for k in _kernel_metadata(obj) if "sqp_group_kernel" in k]
     # <BOUNDED, XB, EXACT>: state-bounded (Gauss-Newton and, round 6, exact) and control-bounded (both Hessians)
-    assert sorted(k.split("TwoLinkArmE")[1][:14] for k in kernels) == \
+    assert sorted(k.split("TwoLinkArmE")[1][:12] for k in kernels) == \
         ["Lb0ELb1ELb0E", "Lb0ELb1ELb1E", "Lb1ELb0ELb0E", "Lb1ELb0ELb1E"], kernels
     r = _rules(os.path.join(AMD, "Makefile"))
     assert any("$(LANEFLAGS)" in l and "MMPC_GROUP_BOUNDED_UNIT" in l for l in r["build/group_two_link_bounded.o"])
