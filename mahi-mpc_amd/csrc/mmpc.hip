@@ -748,6 +748,7 @@ int launch_group(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const So
 
 // Riccati workspace (sqp_lane.h / sqp_group.h layouts), grown on demand.  Growth is synchronous:
 // hipFree waits for the kernels still using the old buffer.
+constexpr size_t kExitCountBytes = 256;
 int ensure_workspace_bytes(mmpc_handle* h, size_t bytes, double** out) {
     int dev = -1;
     MMPC_HIP(hipGetDevice(&dev));
@@ -757,7 +758,9 @@ int ensure_workspace_bytes(mmpc_handle* h, size_t bytes, double** out) {
         if (h->ws) MMPC_HIP(hipFree(h->ws));
         h->ws = nullptr;
         h->ws_bytes = 0;
-        MMPC_HIP(hipMalloc(reinterpret_cast<void**>(&h->ws), bytes));
+        // + the 16-lane kernel's finish counter (SolveParams::exit_count), zeroed once here and reset by every launch
+        MMPC_HIP(hipMalloc(reinterpret_cast<void**>(&h->ws), bytes + kExitCountBytes));
+        MMPC_HIP(hipMemset(reinterpret_cast<char*>(h->ws) + bytes, 0, kExitCountBytes));
         h->ws_bytes = bytes;
         h->ws_dev = dev;
     }
@@ -888,6 +891,7 @@ int launch_solve(mmpc_handle* h, int64_t B, const double* x0, const double* u_pr
     p.tail_lws_block = 0;
     p.tail_lws_ss = p.tail_lws_zl = 0;
     p.gpw = kGroupsPerWave;
+    p.exit_count = nullptr;
     // any bound pointer selects the kernels' BOUNDED variant (projected GN-SQP, sqp_wave.h); host entry
     // points pass NULL for bounds that are all infinite
     const bool bounded = u_lb || u_ub;
@@ -920,14 +924,14 @@ int launch_kernel(mmpc_handle* h, int solver, const SolveParams& p, bool bounded
         dim3 grid(grid1d(B, kGroupsPerWave)), block(64);
         const int hess = resolve_hessian(h, solver, bounded);
         if (hess < 0) return hess;
-#ifdef MMPC_GROUP_HOLD_EXIT
-        static int32_t* hold_ctr = nullptr;   // diagnostic A/B build only (sqp_group.h)
-        if (!hold_ctr) MMPC_HIP(hipMalloc(&hold_ctr, 256));
-        MMPC_HIP(hipMemsetAsync(hold_ctr, 0, sizeof(int32_t), stream));
         SolveParams pg = p;
-        pg.tail_count = hold_ctr;
-#else
-        const SolveParams& pg = p;
+#if MMPC_GROUP_EXIT_HOLD
+        // resident finish: when the whole grid is resident at once (one wave per SIMD by registers, the
+        // workgroups per CU the LDS allows), finished waves stay resident until the launch's last waves have finished
+        if ((rc = query_cu_count(h))) return rc;
+        const int64_t resident = static_cast<int64_t>(h->cu_count) * std::min<int64_t>(4, (160 * 1024) / std::max<size_t>(lds, 1));
+        if (grid.x >= 2 && static_cast<int64_t>(grid.x) <= resident)
+            pg.exit_count = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(lw.ws) + h->ws_bytes);
 #endif
         rc = with_model(mi.model_id, [&](auto* m) {
             using M = std::remove_pointer_t<decltype(m)>;

@@ -30,6 +30,9 @@ namespace mmpc {
 #endif
 // A/B switch (round 6, diagnostic builds): the W_k and [K_k | kff_k] records go to the HBM workspace with
 // non-temporal stores (no L2 allocation) instead of plain ones
+#ifndef MMPC_GROUP_EXIT_HOLD   // resident finish of the 16-lane kernel; 0: waves exit as they finish
+#define MMPC_GROUP_EXIT_HOLD 0
+#endif
 #ifndef MMPC_GROUP_WB_COALESCED   // A/B switch: V written back 16 consecutive doubles per store instruction
 #define MMPC_GROUP_WB_COALESCED 0
 #endif
@@ -178,6 +181,12 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     const int gi = threadIdx.x / G;
     [[maybe_unused]] const int lane0 = threadIdx.x;
     MMPC_PHASE_DECL
+#ifdef MMPC_GROUP_SLEEP_EXIT
+    const unsigned long long sl_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+#if MMPC_GROUP_EXIT_HOLD
+    const unsigned long long fin_t0 = __builtin_amdgcn_s_memrealtime();   // resident finish: this wave's start
+#endif
     const int gbase = gi * G;  // first lane of this instance's group
     // slot of this group in the launch: the instance itself, or (resume launch, p.tail_idx) an entry of the lane
     // kernel's hand-over list
@@ -1891,14 +1900,45 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     }
     MMPC_PHASE(7);
     MMPC_PHASE_FLUSH
-#ifdef MMPC_GROUP_HOLD_EXIT
-    // diagnostic A/B (lib_var builds only): a finished wave stays resident, sleeping, until every wave of the launch
-    // has finished (bounded wait), so no wave of a solve runs while others of the launch have already left
-    if (!resume && p.tail_count) {
-        if (threadIdx.x == 0) atomicAdd(p.tail_count, 1);
-        for (int spins = 0; spins < 50000; ++spins) {
-            if (__hip_atomic_load(p.tail_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (int)gridDim.x) break;
-            __builtin_amdgcn_s_sleep(8);
+#ifdef MMPC_GROUP_SLEEP_EXIT
+    // diagnostic A/B (lib_var builds only): a finished wave sleeps MMPC_GROUP_SLEEP_EXIT % of its own duration before
+    // it exits (s_memrealtime, no memory traffic), so the chip stays occupied while the waves of the last iteration run
+    {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long until = t1 + (t1 - sl_t0) * MMPC_GROUP_SLEEP_EXIT / 100;
+#ifdef MMPC_GROUP_SPIN_EXIT   // ... busy with FP64 FMAs instead of sleeping (the power draw of a running wave)
+        double sp = (double)threadIdx.x;
+        while (__builtin_amdgcn_s_memrealtime() < until) {
+            for (int i = 0; i < 64; ++i) sp = fma(sp, 0.999, 1e-3);
+            asm volatile("" : "+v"(sp));
+        }
+#else
+        while (__builtin_amdgcn_s_memrealtime() < until) __builtin_amdgcn_s_sleep(32);
+#endif
+    }
+#endif
+#if MMPC_GROUP_EXIT_HOLD
+    // resident finish: a wave that finishes while other waves of the launch still run stays resident,
+    // sleeping, until at most 1/32 of the launch's waves are still running (or, a bound, half its own duration has
+    // passed).  Waves that ran on a chip whose other waves had left ran their last iteration up to ~1.5x slower
+    // (cfg#2 at tol 1e-5, profiles/r06/sleep).  One atomic per wave; the wave that finishes last resets the counter
+    // for the next launch; polls every ~2 us (s_sleep, no traffic in between).
+    if (!resume && p.exit_count) {
+        int done_before = 0;
+        if (threadIdx.x == 0) done_before = atomicAdd(p.exit_count, 1);
+        done_before = __builtin_amdgcn_readfirstlane(done_before);   // lane 0 (group 0 of a wave is always valid)
+        const int waves = (int)gridDim.x;
+        if (done_before + 1 >= waves) {
+            if (threadIdx.x == 0) __hip_atomic_store(p.exit_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            const unsigned long long until = t1 + (t1 - fin_t0) / 2;
+            const int leave = waves - max(1, waves / 32);   // finished count at which the waiting waves leave
+            while (__builtin_amdgcn_s_memrealtime() < until) {
+                __builtin_amdgcn_s_sleep(64);
+                const int n = __hip_atomic_load(p.exit_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (n == 0 || n >= leave) break;   // 0: the last wave has reset it
+            }
         }
     }
 #endif

@@ -44,6 +44,18 @@
 #ifndef MMPC_LANE_WPE32
 #define MMPC_LANE_WPE32 1
 #endif
+#ifndef MMPC_LANE_C_RECOMPUTE   // step sweep: c_k from its own model evaluation instead of the stored C (round 6)
+#define MMPC_LANE_C_RECOMPUTE 1
+#endif
+#ifndef MMPC_LANE_C_NOSTORE   // no C record: the backward sweep recomputes c_k too (requires MMPC_LANE_C_RECOMPUTE)
+#define MMPC_LANE_C_NOSTORE 1
+#endif
+#ifndef MMPC_LANE_LAZY_DXU   // unbounded solves: DX / DU stored in the first iteration only (regenerated on demand)
+#define MMPC_LANE_LAZY_DXU 1
+#endif
+#ifndef MMPC_LANE_XTRA_K
+#define MMPC_LANE_XTRA_K 0
+#endif
 #ifndef MMPC_LANE_XB_EARLY
 #define MMPC_LANE_XB_EARLY 1
 #endif
@@ -486,7 +498,7 @@ sqp_lane_kernel(SolveParams p,
                 for (int r = 0; r < NX; ++r) {
                     const double F = fma(h, xd[r], xk[r]);
                     const double c = F - xn[r];
-                    SK(0, SF::C, r) = c;
+                    if constexpr (!MMPC_LANE_C_NOSTORE) SK(0, SF::C, r) = c;
                     cmax = fmax(cmax, fabs(c));
                     c1 += fabs(c);
                     nonfinite |= !isfinite(c);
@@ -529,6 +541,12 @@ sqp_lane_kernel(SolveParams p,
         double gmax = 0.0, lmax = 0.0, dJ = 0.0;
         double mub_next = mub, amax = 1.0, az = 1.0, dbar = 0.0;  // interior point (XB)
         bool fact_ok = true, done = false;
+        // lazy step records (round 6): an unbounded solve's step sweep stores dx_k / du_k (DX / DU) only in the first
+        // iteration; later the full step is nearly always taken (cfg#3: every instance-iteration after the first,
+        // profiles/r03/alpha_stats_cfg3_v1.json), and a lane whose full step is rejected regenerates them (same
+        // expressions, same bits) before its first shorter trial
+        const bool wdxu = !(SWAP && MMPC_LANE_LAZY_DXU) || it == 0;
+        bool have_dxu = wdxu;
         fwd_ready = false;
         const double beps = BOUNDED ? fmin(kBoundEps, pg_prev) : 0.0;
         double Jt1 = 0.0, ct1 = 0.0, cmt1 = 0.0;
@@ -700,8 +718,12 @@ sqp_lane_kernel(SolveParams p,
                     unext[c] = 0.0;
                     upf[c] = ST(N - 1, FU, c);
                 }
+                double xk1[NX];   // x_{k+1} (MMPC_LANE_C_NOSTORE)
 #pragma unroll
-                for (int r = 0; r < NX; ++r) xpf[r] = ST(N - 1, FX, r);
+                for (int r = 0; r < NX; ++r) {
+                    xpf[r] = ST(N - 1, FX, r);
+                    xk1[r] = ST(N, FX, r);
+                }
                 #pragma unroll 1
                 for (int k = N - 1; k >= 0; --k) {
                     gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
@@ -710,7 +732,7 @@ sqp_lane_kernel(SolveParams p,
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         x[r] = xpf[r];
-                        cc[r] = SK(0, SF::C, r);
+                        if constexpr (!MMPC_LANE_C_NOSTORE) cc[r] = SK(0, SF::C, r);
                         dk[r] = SK(0, SF::D, r);
                     }
 #pragma unroll
@@ -759,6 +781,16 @@ sqp_lane_kernel(SolveParams p,
                     auto xb_sgx = [&](int r) { if constexpr (XE) return sgx[r]; else return (double)SK(-1, SF::SG, r); };
                     auto xb_bbx = [&](int r) { if constexpr (XE) return bbx[r]; else return (double)SK(-1, SF::BB, r); };
                     STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                    if constexpr (MMPC_LANE_C_NOSTORE) {
+                        // c_k = F(x_k, u_k) - x_{k+1} from this sweep's own evaluation (round 6: no C record in the
+                        // workspace; the Jacobian evaluation's value is pass (1)'s bit for bit on cfg#3/#5, exact, |u|
+                        // <= 0.5: profiles/r06/cns)
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) {
+                            cc[r] = fma(h, xd[r], x[r]) - xk1[r];
+                            xk1[r] = x[r];
+                        }
+                    }
                     // exact Hessian: W_k at (x_k, u_k) with lam_{k+1} (lam holds it until the adjoint step below)
                     constexpr int KZ = NX + NU;
                     double Wk[EXACT ? KZ * KZ : 1];
@@ -1210,7 +1242,7 @@ sqp_lane_kernel(SolveParams p,
                         x[r] = xpf[r];
                         xpf[r] = SK(1, FX, r);
                         rk[r] = SK(0, SF::R, r);
-                        ck[r] = SK(0, SF::C, r);
+                        if constexpr (!MMPC_LANE_C_RECOMPUTE) ck[r] = SK(0, SF::C, r);
                     }
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
@@ -1242,6 +1274,10 @@ sqp_lane_kernel(SolveParams p,
 #pragma unroll
                         for (int e = 0; e < NU * NS; ++e) kv[e] = kk[e * 64];
                         __builtin_amdgcn_sched_barrier(0);
+#if MMPC_LANE_XTRA_K   // diagnostic A/B only: the gains stored back (same values): + the K record's write traffic
+#pragma unroll
+                        for (int e = 0; e < NU * NS; ++e) ((gmem<FT>*)kk)[e * 64] = kv[e];
+#endif
 #pragma unroll
                         for (int a = 0; a < NU; ++a) {
                             const int base = a * NS;
@@ -1251,7 +1287,7 @@ sqp_lane_kernel(SolveParams p,
 #pragma unroll
                             for (int c = 0; c < NU; ++c) t = fma((double)kv[base + NX + c], dup[c], t);
                             du[a] = t;
-                            SK(0, SF::DU, a) = t;
+                            if (wdxu) SK(0, SF::DU, a) = t;
                         }
                     } else {
                         // loads at their uses (MMPC_LANE_XB_BATCHED=0 only).  The batched form above computed wrong
@@ -1297,10 +1333,14 @@ sqp_lane_kernel(SolveParams p,
 #pragma unroll
                     for (int r = 0; r < NX; ++r) {
                         const double F = fma(h, xd[r], x[r]);
+                        // c_k = F(x_k, u_k) - x_{k+1} from this evaluation: the stored C_k is the same expression of the
+                        // same model function at the same point (pass (1) or the previous iteration's fused trial), so
+                        // the same bits, without its load (round 6)
+                        if constexpr (MMPC_LANE_C_RECOMPUTE) ck[r] = F - xpf[r];
                         const double qe = 2.0 * Q[r] * (F - rk[r]);
                         dJ = fma(qe, ad[r], dJ);
                         dx[r] = ad[r] + ck[r];
-                        SK(1, SF::DX, r) = dx[r];
+                        if (wdxu) SK(1, SF::DX, r) = dx[r];
                     }
 #pragma unroll
                     for (int c = 0; c < NU; ++c) {
@@ -1337,7 +1377,7 @@ sqp_lane_kernel(SolveParams p,
                                 const double xn1 = xpf[r] + dx[r];   // x_{k+1} + dx_{k+1}: the update's fma(1, dx, x)
                                 if constexpr (SWAP) SK(1, FXo, r) = xn1;
                                 const double c = F - xn1;
-                                SK(0, SF::C, r) = c;
+                                if constexpr (!MMPC_LANE_C_NOSTORE) SK(0, SF::C, r) = c;
                                 cmt1 = fmax(cmt1, fabs(c));
                                 ct1 += fabs(c);
                                 nft1 |= !isfinite(c);
@@ -1404,6 +1444,62 @@ sqp_lane_kernel(SolveParams p,
                 Jt = Jt1;
                 ct = ct1;
             } else {
+            if constexpr (SWAP && MMPC_LANE_LAZY_DXU) {
+                if (!have_dxu) {   // the step sweep's du_k, dx_{k+1} again (its expressions, in its order), stored
+                    double dx[NX], dup[NU];
+#pragma unroll
+                    for (int r = 0; r < NX; ++r) dx[r] = 0.0;
+#pragma unroll
+                    for (int c = 0; c < NU; ++c) dup[c] = 0.0;
+                    #pragma unroll 1
+                    for (int k = 0; k < N; ++k) {
+                        gmem<double>* const sk = stage_ptr(wsb, k, SS, lane);
+                        double x[NX], u[NU], xn[NX], xd[NX], du[NU], ad[NX];
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) {
+                            x[r] = SK(0, FX, r);
+                            xn[r] = SK(1, FX, r);
+                        }
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) u[c] = SK(0, FU, c);
+                        const gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
+                        const gmem<FT>* const kk = (const gmem<FT>*)(kb + NU * 64) + lane;
+#pragma unroll
+                        for (int a = 0; a < NU; ++a) {
+                            const int base = a * NS;
+                            double t = kb[a * 64 + lane];
+#pragma unroll
+                            for (int q = 0; q < NX; ++q) t = fma((double)kk[(base + q) * 64], dx[q], t);
+#pragma unroll
+                            for (int c = 0; c < NU; ++c) t = fma((double)kk[(base + NX + c) * 64], dup[c], t);
+                            du[a] = t;
+                            SK(0, SF::DU, a) = t;
+                        }
+                        if (JVP && !lin) {
+                            double jv[NA];
+                            model_jvp<Model>(x, u, dx, du, xd, jv);
+                            jvp_step<NQ, NA>(h, dx, jv, ad);
+                        } else {
+                            double hFq[SQ], hFqd[NA * NA], hFu[NA * NU];
+                            STAGE_EVAL(x, u, xd, hFq, hFqd, hFu, true);
+                            a_mul<NQ, NA>(h, hFq, hFqd, dx, ad);
+#pragma unroll
+                            for (int s2 = 0; s2 < NA; ++s2)
+#pragma unroll
+                                for (int c = 0; c < NU; ++c) ad[NQ + s2] = fma(hFu[s2 * NU + c], du[c], ad[NQ + s2]);
+                        }
+#pragma unroll
+                        for (int r = 0; r < NX; ++r) {
+                            const double F = fma(h, xd[r], x[r]);
+                            dx[r] = ad[r] + (F - xn[r]);
+                            SK(1, SF::DX, r) = dx[r];
+                        }
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) dup[c] = du[c];
+                    }
+                    have_dxu = true;
+                }
+            }
 #pragma unroll
             for (int r = 0; r < NX; ++r) xk[r] = ST(0, FX, r);  // dx_0 = 0
 #pragma unroll

@@ -81,6 +81,10 @@ struct SolveParams {
     int tail_lws_ss;         // doubles per stage (x 64 lanes)
     int tail_lws_zl;         // field offset of z_l; z_u follows at + nx + nu
     int gpw;               // 16-lane kernel: instance groups per wave of this launch (kGroupsPerWave, or fewer)
+    // 16-lane kernel, launches whose grid is resident at once (DESIGN.md 4c "resident finish"): waves count themselves
+    // out here when they finish and stay resident, sleeping, while other waves of the launch still run; the last one
+    // resets it to 0.  nullptr: waves exit as they finish
+    int32_t* exit_count;
 };
 // instance status while handed over (never returned: the resume launch overwrites it)
 constexpr int ST_HANDED_OVER = 6;
