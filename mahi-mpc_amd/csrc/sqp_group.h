@@ -33,6 +33,9 @@ namespace mmpc {
 #ifndef MMPC_GROUP_EXIT_HOLD   // resident finish of the 16-lane kernel; 0: waves exit as they finish
 #define MMPC_GROUP_EXIT_HOLD 0
 #endif
+#ifndef MMPC_GROUP_WZERO_ONCE   // W_k's structural zeros stored once per launch (w_struct_zero)
+#define MMPC_GROUP_WZERO_ONCE 1
+#endif
 #ifndef MMPC_GROUP_WB_COALESCED   // A/B switch: V written back 16 consecutive doubles per store instruction
 #define MMPC_GROUP_WB_COALESCED 0
 #endif
@@ -44,6 +47,13 @@ __device__ __forceinline__ void ws_store(T* p, T v) {
     if constexpr (MMPC_GROUP_NT_STORES) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
+// Entries of W_k's x rows that Model::eval_hess always leaves 0 (structural zeros): a launch stores them in its first
+// W pass only (MMPC_GROUP_WZERO_ONCE, round 6).  2-link arm (two_link_fast.h eval_hess: q_A enters only through
+// gravity, the torques linearly): row 0 is zero in columns 2..5, rows 2 and 3 in columns 0, 4 and 5.
+template <class Model>
+__device__ constexpr bool w_struct_zero(int, int) { return false; }
+template <>
+__device__ constexpr bool w_struct_zero<TwoLinkArm>(int r, int j) { return (r == 0 && j >= 2) || (r >= 2 && (j == 0 || j >= 4)); }
 constexpr int kGroupLanes = 16;
 constexpr int kGroupsPerWave = 4;
 
@@ -224,6 +234,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
     double* const wH = wK + N * NU * (NS + 1);  // EXACT: [N][HW] = W_k x rows [NX][KZ] | W_k uu block [NU][NU]
     constexpr int NR = NS + NU + 1;             // BOUNDED: [N][NU][NR] = un-held [H_wx | -R | H_ww | h_w] rows
     double* const wRel = wH + N * HW;
+    bool w_zeros_stored = false;   // W_k's structural zeros are in the workspace (this launch's first W pass stored them)
     // interior point (XB): per stage k, y = (x_{k+1} | u_k) [NY]: duals z_l, z_u, Sigma, b, z_u - z_l -- in the HBM
     // workspace after the W blocks (group_lds_doubles); the stage-parallel phases write them, the serial sweeps read
     // them on other lanes after a workgroup fence
@@ -1512,7 +1523,9 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
 #pragma unroll
                 for (int r2 = 0; r2 < NX; ++r2)
 #pragma unroll
-                    for (int j = 0; j < KZ; ++j) ws_store(&dst[r2 * KZ + j], W[r2 * KZ + j]);
+                    for (int j = 0; j < KZ; ++j)
+                        if (!(MMPC_GROUP_WZERO_ONCE && w_struct_zero<Model>(r2, j)) || !w_zeros_stored)
+                            ws_store(&dst[r2 * KZ + j], W[r2 * KZ + j]);
                 if constexpr (!CAFF) {
 #pragma unroll
                     for (int a = 0; a < NU; ++a)
@@ -1520,6 +1533,7 @@ __global__ __launch_bounds__(64) void sqp_group_kernel(SolveParams p, GroupWork 
                         for (int b = 0; b < NU; ++b) ws_store(&dst[NX * KZ + a * NU + b], W[(NX + a) * KZ + NX + b]);
                 }
             }
+            w_zeros_stored = true;
             MMPC_PHASE(9);   // (timing build: "check" = the stop test and this W pass up to its fence)
             // the stores of the other lanes of this wave must be visible to the sweep's loads
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
