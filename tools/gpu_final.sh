@@ -20,6 +20,7 @@ if [ -z "$SKIP_PMC" ]; then
   OUT="$OUT/pmc" bash tools/gpu_pmc_all.sh || exit 1
   cp "$OUT/pmc/traffic_latest.json" profiles/traffic_latest.json
 fi
+[ -n "$SKIP_BENCH" ] && { echo "pmc done (SKIP_BENCH)"; exit 0; }
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$OUT/bench_default.json" 2> "$OUT/bench_default.err" || { tail -20 "$OUT/bench_default.err"; exit 1; }
 echo "bench ok"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_default" -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/prof_default.json" 2> "$OUT/prof_default.err" || { tail -20 "$OUT/prof_default.err"; exit 1; }
