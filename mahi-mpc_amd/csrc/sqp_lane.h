@@ -53,6 +53,9 @@
 #ifndef MMPC_LANE_LAZY_DXU   // unbounded solves: DX / DU stored in the first iteration only (regenerated on demand)
 #define MMPC_LANE_LAZY_DXU 1
 #endif
+#ifndef MMPC_LANE_KPACK   // gain record with H_ww^-1 instead of K_u (kgain_idx; not for control-bounded solves)
+#define MMPC_LANE_KPACK 1
+#endif
 #ifndef MMPC_LANE_XTRA_K
 #define MMPC_LANE_XTRA_K 0
 #endif
@@ -123,6 +126,18 @@ struct LaneWork {
 __host__ __device__ constexpr int sym_idx(int n, int i, int j) {
     return i <= j ? i * n - i * (i - 1) / 2 + (j - i) : j * n - j * (j - 1) / 2 + (i - j);
 }
+
+// Gain record [K_k] after kff_k (round 6, KPACK): K_x row-major [NU][NX], then H_ww^-1 packed (sym_idx): K_u =
+// -H_ww^-1 (-R) = H_ww^-1 diag(R), so the step sweep forms K_u du_{k-1} as H_ww^-1 (R o du_{k-1}) from 10 stored
+// values instead of 16 (exo).  Not for control-bounded solves (held rows change K_u).  Otherwise [NU][NX + NU].
+template <int NX, int NU, bool KPACK>
+__host__ __device__ constexpr int kgain_idx(int a, int j) {
+    return !KPACK    ? a * (NX + NU) + j
+           : j < NX ? a * NX + j
+                    : NU * NX + sym_idx(NU, a < j - NX ? a : j - NX, a < j - NX ? j - NX : a);
+}
+template <int NX, int NU, bool KPACK>
+__host__ __device__ constexpr int kgain_count() { return KPACK ? NU * NX + NU * (NU + 1) / 2 : NU * (NX + NU); }
 
 // The P~_xu / P~_uu entries of the packed P~ are dead once G, H_ww, h_w and Y of a Riccati step are formed: their
 // slots hold the rows NQ..NX-1 of W = P_xx A (NA x NX) while P~_xx is rebuilt in place (sqp_lane_kernel, "W in
@@ -252,6 +267,11 @@ sqp_lane_kernel(SolveParams p,
     // the other, which the step sweep fills with the full-step point (x_k + dx_k, u_k + du_k) -- an accepted full step
     // (99.7 % of the cfg#3 iterations) swaps the names instead of running the update pass over the workspace
     constexpr bool SWAP = !BOUNDED && !XB;
+    constexpr bool KPACK = !BOUNDED && MMPC_LANE_KPACK;   // gain record layout (kgain_idx)
+    // lazy step records (DX / DU, below): unbounded solves; not with the exact Hessian, whose kernel ran 11.19 -> 11.74 ms
+    // with them (cfg#3 exact, the regeneration's registers: profiles/r06/kpack/abx)
+    constexpr bool LAZY = SWAP && !EXACT && MMPC_LANE_LAZY_DXU;
+    constexpr int KN = kgain_count<NX, NU, KPACK>();
     int FX = SF::X, FU = SF::U, FXo = SWAP ? SF::X1 : SF::X, FUo = SWAP ? SF::U1 : SF::U;
 
     const double* w = p.weights + inst * p.w_stride;
@@ -545,7 +565,7 @@ sqp_lane_kernel(SolveParams p,
         // iteration; later the full step is nearly always taken (cfg#3: every instance-iteration after the first,
         // profiles/r03/alpha_stats_cfg3_v1.json), and a lane whose full step is rejected regenerates them (same
         // expressions, same bits) before its first shorter trial
-        const bool wdxu = !(SWAP && MMPC_LANE_LAZY_DXU) || it == 0;
+        const bool wdxu = !LAZY || it == 0;
         bool have_dxu = wdxu;
         fwd_ready = false;
         const double beps = BOUNDED ? fmin(kBoundEps, pg_prev) : 0.0;
@@ -1030,7 +1050,7 @@ sqp_lane_kernel(SolveParams p,
 #pragma unroll
                         for (int a = 0; a < NU; ++a) kb[a * 64 + lane] = -kh[a];
 #pragma unroll
-                        for (int j = 0; j < NS; ++j) {
+                        for (int j = 0; j < (KPACK ? NX : NS); ++j) {
                             FT kc[NU];
 #pragma unroll
                             for (int a = NU - 1; a >= 0; --a) {
@@ -1040,7 +1060,28 @@ sqp_lane_kernel(SolveParams p,
                                 kc[a] = t * il[a];
                             }
 #pragma unroll
-                            for (int a = 0; a < NU; ++a) kk[(a * NS + j) * 64] = -kc[a];
+                            for (int a = 0; a < NU; ++a) kk[kgain_idx<NX, NU, KPACK>(a, j) * 64] = -kc[a];
+                        }
+                        if constexpr (KPACK) {   // H_ww^-1 column c, rows a >= c: L^-T (L^-1 e_c)
+#pragma unroll
+                            for (int c = 0; c < NU; ++c) {
+                                FT z[NU], hc[NU];
+#pragma unroll
+                                for (int q = c; q < NU; ++q) {
+                                    FT t = q == c ? (FT)1 : (FT)0;
+#pragma unroll
+                                    for (int m = c; m < q; ++m) t = fma(-Ld[q][m], z[m], t);
+                                    z[q] = t * il[q];
+                                }
+#pragma unroll
+                                for (int a = NU - 1; a >= c; --a) {
+                                    FT t = z[a];
+#pragma unroll
+                                    for (int q = a + 1; q < NU; ++q) t = fma(-Ld[q][a], hc[q], t);
+                                    hc[a] = t * il[a];
+                                    kk[kgain_idx<NX, NU, KPACK>(a, NX + c) * 64] = hc[a];
+                                }
+                            }
                         }
                     }
                     if (k == 0) break;  // s_0 = 0: P~_0 is never used
@@ -1267,25 +1308,27 @@ sqp_lane_kernel(SolveParams p,
                     if constexpr (!XB || MMPC_LANE_XB_BATCHED) {
                         // all loads of [K_k | kff_k] issued before the first use: under register pressure the
                         // scheduler otherwise interleaves load -> vmcnt(0) -> fma, one memory round trip per gain
-                        FT kv[NU * NS];
+                        FT kv[KN];
                         double kf[NU];
 #pragma unroll
                         for (int a = 0; a < NU; ++a) kf[a] = kb[a * 64 + lane];
 #pragma unroll
-                        for (int e = 0; e < NU * NS; ++e) kv[e] = kk[e * 64];
+                        for (int e = 0; e < KN; ++e) kv[e] = kk[e * 64];
                         __builtin_amdgcn_sched_barrier(0);
 #if MMPC_LANE_XTRA_K   // diagnostic A/B only: the gains stored back (same values): + the K record's write traffic
 #pragma unroll
-                        for (int e = 0; e < NU * NS; ++e) ((gmem<FT>*)kk)[e * 64] = kv[e];
+                        for (int e = 0; e < KN; ++e) ((gmem<FT>*)kk)[e * 64] = kv[e];
 #endif
+                        double dr[NU];   // the vector K_u multiplies: du_{k-1}, or R o du_{k-1} (KPACK)
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) dr[c] = KPACK ? R[c] * dup[c] : dup[c];
 #pragma unroll
                         for (int a = 0; a < NU; ++a) {
-                            const int base = a * NS;
                             double t = kf[a];
 #pragma unroll
-                            for (int q = 0; q < NX; ++q) t = fma((double)kv[base + q], dx[q], t);
+                            for (int q = 0; q < NX; ++q) t = fma((double)kv[kgain_idx<NX, NU, KPACK>(a, q)], dx[q], t);
 #pragma unroll
-                            for (int c = 0; c < NU; ++c) t = fma((double)kv[base + NX + c], dup[c], t);
+                            for (int c = 0; c < NU; ++c) t = fma((double)kv[kgain_idx<NX, NU, KPACK>(a, NX + c)], dr[c], t);
                             du[a] = t;
                             if (wdxu) SK(0, SF::DU, a) = t;
                         }
@@ -1297,12 +1340,12 @@ sqp_lane_kernel(SolveParams p,
                         // 92.4 -> 74.3 ms (round 4, profiles/r04/ab_xbb).
 #pragma unroll
                         for (int a = 0; a < NU; ++a) {
-                            const int base = a * NS;
                             double t = kb[a * 64 + lane];
 #pragma unroll
-                            for (int q = 0; q < NX; ++q) t = fma((double)kk[(base + q) * 64], dx[q], t);
+                            for (int q = 0; q < NX; ++q) t = fma((double)kk[kgain_idx<NX, NU, KPACK>(a, q) * 64], dx[q], t);
 #pragma unroll
-                            for (int c = 0; c < NU; ++c) t = fma((double)kk[(base + NX + c) * 64], dup[c], t);
+                            for (int c = 0; c < NU; ++c)
+                                t = fma((double)kk[kgain_idx<NX, NU, KPACK>(a, NX + c) * 64], KPACK ? R[c] * dup[c] : dup[c], t);
                             du[a] = t;
                             SK(0, SF::DU, a) = t;
                         }
@@ -1444,7 +1487,7 @@ sqp_lane_kernel(SolveParams p,
                 Jt = Jt1;
                 ct = ct1;
             } else {
-            if constexpr (SWAP && MMPC_LANE_LAZY_DXU) {
+            if constexpr (LAZY) {
                 if (!have_dxu) {   // the step sweep's du_k, dx_{k+1} again (its expressions, in its order), stored
                     double dx[NX], dup[NU];
 #pragma unroll
@@ -1464,14 +1507,16 @@ sqp_lane_kernel(SolveParams p,
                         for (int c = 0; c < NU; ++c) u[c] = SK(0, FU, c);
                         const gmem<double>* const kb = stage_ptr(wsb, k, SS, 0) + SF::K * 64;
                         const gmem<FT>* const kk = (const gmem<FT>*)(kb + NU * 64) + lane;
+                        double dr[NU];
+#pragma unroll
+                        for (int c = 0; c < NU; ++c) dr[c] = KPACK ? R[c] * dup[c] : dup[c];
 #pragma unroll
                         for (int a = 0; a < NU; ++a) {
-                            const int base = a * NS;
                             double t = kb[a * 64 + lane];
 #pragma unroll
-                            for (int q = 0; q < NX; ++q) t = fma((double)kk[(base + q) * 64], dx[q], t);
+                            for (int q = 0; q < NX; ++q) t = fma((double)kk[kgain_idx<NX, NU, KPACK>(a, q) * 64], dx[q], t);
 #pragma unroll
-                            for (int c = 0; c < NU; ++c) t = fma((double)kk[(base + NX + c) * 64], dup[c], t);
+                            for (int c = 0; c < NU; ++c) t = fma((double)kk[kgain_idx<NX, NU, KPACK>(a, NX + c) * 64], dr[c], t);
                             du[a] = t;
                             SK(0, SF::DU, a) = t;
                         }

@@ -2,4 +2,4 @@
 # library's sha256 (tools/gpu_final.sh without the bench; its traffic_latest.json goes into profiles/ afterwards)
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/final6 SKIP_BENCH=1 PMC_LABEL_DIR=profiles/r06/final/pmc bash tools/gpu_final.sh
+OUT=gpurun_out/final7 SKIP_BENCH=1 PMC_LABEL_DIR=profiles/r06/final/pmc bash tools/gpu_final.sh

@@ -2,7 +2,7 @@
 # bench line, its rocprofv3 kernel-trace summary, the secondary lines and three tolerance lines
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/final6b; mkdir -p $OUT
+OUT=gpurun_out/final7b; mkdir -p $OUT
 sha256sum mahi-mpc_amd/lib/libmmpc.so > $OUT/lib_sha256.txt
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_default.json 2> $OUT/bench_default.err || { tail -20 $OUT/bench_default.err; exit 1; }
 echo "bench ok"

@@ -20,7 +20,8 @@ W_EXO = np.array([10.0] * 4 + [1.0] * 4 + [1.0] * 4 + [0.01] * 4)
 
 
 # regen: whether this batch has shorter steps after the first iteration (GPU trace, round 6: 2-link Gauss-Newton 1,
-# exo exact 8 instance-iterations; the exo Gauss-Newton batch takes only full steps after the first iteration)
+# exo exact 8 instance-iterations; the exo Gauss-Newton batch takes only full steps after the first iteration).  The
+# exact-Hessian lane kernel keeps storing dx / du every iteration (sqp_lane.h LAZY): its case checks that path.
 @pytest.mark.parametrize("model,N,B,hess,regen", [("two_link_arm", 30, 256, "gn", True), ("exo_arm", 50, 128, "gn", False),
                                                    ("exo_arm", 50, 128, "exact", True)])
 def test_lane_lazy_step_records_vs_oracle(model, N, B, hess, regen, mmpc_mod, oracle, tmp_path):
