@@ -211,7 +211,7 @@ int mmpc_resolve_kkt_solver(const mmpc_handle* h, int64_t B, int32_t* solver);
 /* The Hessian (MMPC_HESSIAN_GAUSS_NEWTON or MMPC_HESSIAN_EXACT) a solve of B instances runs under the handle's
  * options; u_bounded = whether the solve passes control bounds (AUTO resolves control-bounded solves to
  * Gauss-Newton; an explicit EXACT is honoured with control bounds on RICCATI_GROUP and RICCATI).
- * MMPC_ERR_UNSUPPORTED when opts.hessian = EXACT cannot be honoured for that solve (state bounds, other solvers). */
+ * MMPC_ERR_UNSUPPORTED when opts.hessian = EXACT cannot be honoured (CONDENSED, fp32 factor); state bounds: yes. */
 int mmpc_resolve_hessian(const mmpc_handle* h, int64_t B, int32_t u_bounded, int32_t* hessian);
 
 /* Batched SQP solve, DEVICE pointers, stream-ordered.  u_lb/u_ub: device [nu] or NULL
