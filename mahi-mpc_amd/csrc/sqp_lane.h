@@ -56,6 +56,9 @@
 #ifndef MMPC_LANE_KPACK   // gain record with H_ww^-1 instead of K_u (kgain_idx; not for control-bounded solves)
 #define MMPC_LANE_KPACK 1
 #endif
+#ifndef MMPC_LANE_LS_HANDOVER   // a rejected full step after the first iteration is handed to the resume launch
+#define MMPC_LANE_LS_HANDOVER 1
+#endif
 #ifndef MMPC_LANE_XTRA_K
 #define MMPC_LANE_XTRA_K 0
 #endif
@@ -1475,6 +1478,29 @@ sqp_lane_kernel(SolveParams p,
         }
         if (done) break;
         // ---- (4) l1-merit Armijo line search (noise-aware, as sqp_wave.h) ----
+        if constexpr (LAZY && MMPC_LANE_LS_HANDOVER) {
+            // a full step rejected after the first iteration: the instance is handed over as at this iteration's stop
+            // test (iterate, count, merit weight before this update) instead of running its line search, the step
+            // records' regeneration and the extra forward pass with its whole wave waiting (round 6: one such
+            // instance in a cfg#3 batch made the launch 7.4 ms instead of 5.8, profiles/r06/blocks/)
+            if (p.tail_cap > 0 && !lean_off && it >= 1) {
+                const double mu1 = fmax(mu, 4.0 * lmax + 1.0);
+                const double phi0 = fma(mu1, c1, J0), dphi = dJ - mu1 * c1, phit = fma(mu1, ct1, Jt1);
+                const double noise = 1.0 + fabs(phi0);
+                // the line search's test at alpha = 1 (no filter clause after the first iteration)
+                if (!(dphi >= -1e-11 * noise || phit <= phi0 + 1e-4 * dphi + 1e-13 * noise)) {
+                    const int slot = atomicAdd(p.tail_count, 1);
+                    if (slot < p.tail_slots) {
+                        p.tail_idx[slot] = (int32_t)inst;
+                        p.tail_it[slot] = it;
+                        p.tail_mu[slot] = mu;
+                        status = ST_HANDED_OVER;
+                        break;
+                    }
+                    lean_off = true;
+                }
+            }
+        }
         mu = fmax(mu, 4.0 * lmax + 1.0);
         const double phi0 = XB ? fma(mu, c1, fma(-2.0 * mub, lsum, J0)) : fma(mu, c1, J0);
         const double dphi = XB ? dJ + dbar - mu * c1 : dJ - mu * c1;

@@ -68,3 +68,25 @@ def test_lane_lazy_step_records_vs_oracle(model, N, B, hess, regen, mmpc_mod, or
         assert (r["iters"][short] == o["iters"][short]).all(), (r["iters"][short], o["iters"][short])
         assert _rel(r["V"][short], o["V"][short]).max() <= 1e-10
     assert np.array_equal(V.cpu().numpy(), r["V"]) and np.array_equal(iters, r["iters"])   # trace: same iterates
+
+
+@pytest.mark.parametrize("model,N,B,hess", [("two_link_arm", 30, 256, "gn"), ("exo_arm", 50, 128, "exact")])
+def test_lane_line_search_handover_vs_oracle(model, N, B, hess, mmpc_mod, oracle, tmp_path):
+    """The same batches with the default iteration-tail policy: a lane whose full step is rejected after the first
+    iteration is handed to the 16-lane resume launch instead of line-searching in its wave (sqp_lane.h
+    MMPC_LANE_LS_HANDOVER).  The resume launch runs the same SQP from the same iterate, count and merit weight, so the
+    solutions are the oracle's (as every hand-over test: tests/test_gpu_tail.py)."""
+    om = oracle.EXO if model == "exo_arm" else oracle.TWO_LINK
+    w = (W_EXO if model == "exo_arm" else np.array(WEIGHTS_CFG)).copy()
+    nx, nu = (8, 4) if model == "exo_arm" else (4, 2)
+    w[nx:nx + nu] *= 0.01
+    x0, up, tr = oracle.synth(20250213, 0, B, N, H, model=om)
+    tr = np.ascontiguousarray(tr * 20.0)
+    p = mmpc_mod.write_model_json(str(tmp_path / f"{model}_{N}.json"), model, nx, nu, 2000, N, model=model)
+    h = mmpc_mod.HESSIAN_EXACT if hess == "exact" else mmpc_mod.HESSIAN_GAUSS_NEWTON
+    s = mmpc_mod.Solver(p, kkt_solver=2, hessian=h, init_states=mmpc_mod.INIT_ZERO, max_iter=60)
+    r = s.solve_batch_host(x0, up, tr, w)
+    o = oracle.solve_batch(N, H, x0, up, tr, w, model=om, kkt=oracle.KKT_RICCATI, init_states=2, max_iter=60,
+                           hessian=oracle.HESS_EXACT if hess == "exact" else oracle.HESS_GAUSS_NEWTON)
+    assert (r["status"] == 0).all() and (o["status"] == 0).all()
+    _compare(r, o)
